@@ -1,0 +1,156 @@
+/*
+ * mmni.h — C ABI of the MI355X-native hot path of Transconnectome/multimodal_neuroimage.
+ *
+ * One shared library, libmmni.so (built for gfx950 by __graft_entry__.build()), exports
+ * every entry point below.  The ABI is plain C: device pointers, sizes, strides and a
+ * hipStream_t passed as void*.  No torch types cross it.  The library never allocates
+ * or frees device memory; outputs, saved-for-backward tensors and gradient accumulators
+ * are allocated by the caller (PyTorch on the Python side) and zeroed where documented.
+ *
+ * Error convention: every int-returning function returns
+ *   0  on success,
+ *  <0  for a bad argument (shape / stride / unsupported template combination),
+ *  >0  a hipError_t from the launch.
+ * mmni_last_error() returns a thread-local message describing the last failure.
+ *
+ * Streams: every launch goes to the caller's stream (torch.cuda.current_stream()).
+ * Nothing synchronises the device; every entry point is graph-capturable.
+ *
+ * Reference interfaces each entry point replaces are cited per function
+ * (paths relative to the reference repository root).
+ */
+#ifndef MMNI_H
+#define MMNI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMNI_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------------------
+ * Shifted-window attention.
+ *
+ * Token layout in HBM: channels-last (B, D, H, W, channels); token row
+ *   row(b, z, y, x) = ((b*D + z)*H + y)*W + x.
+ * The cyclic shift (torch.roll by -shift) and window partition of
+ *   modules/swin_v2_module.py:35-46,278  and  modules/swinfusion_module.py:33-45,351
+ * are folded into the kernels' addressing: window w = ((b*nWd + wz)*nWh + wy)*nWw + wx,
+ * window-local token t = (i*wh + j)*ww + k reads row(b, (wz*wd+i+sd)%D, (wy*wh+j+sh)%H,
+ * (wx*ww+k+sw)%W); outputs are written back to the same row, which is exactly the
+ * reverse partition + reverse roll (swinfusion_module.py:366-373).
+ * 2D reference shapes use D = 1, wd = 1, sd = 0.
+ *
+ * Element (row, head h, channel c) of q / k / v lives at  ptr[row*stride + h*head_dim + c];
+ * a packed qkv projection (B*L, 3C) is passed as q = base, k = base + C, v = base + 2C
+ * with all strides 3C; the cross-attention kv projection (B*L, 2C) as k = kv, v = kv + C.
+ * ------------------------------------------------------------------------------------ */
+typedef struct mmni_wattn_desc {
+    int32_t B;                  /* volumes in the batch                                   */
+    int32_t D, H, W;            /* spatial extents (D = 1 for the 2D reference shapes)    */
+    int32_t C;                  /* channels = heads * head_dim                            */
+    int32_t heads;
+    int32_t wd, wh, ww;         /* window extent per axis                                 */
+    int32_t sd, sh, sw;         /* cyclic shift per axis; 0 = unshifted (no mask)         */
+    int32_t kind;               /* 0: SwinFusion scaled dot product + learned table bias
+                                      (swinfusion_module.py:114-145, 213-246)
+                                   1: Swin-V2 cosine attention, tau per head
+                                      (swin_v2_module.py:138-178)                         */
+    float   scale;              /* kind 0: q scale (head_dim^-0.5); ignored for kind 1    */
+    int64_t q_stride;           /* elements between consecutive token rows of q           */
+    int64_t k_stride;
+    int64_t v_stride;
+    int64_t o_stride;           /* output rows (and dq/dk/dv rows use q/k/v strides)      */
+} mmni_wattn_desc;
+
+/* Forward.  table: (Tsz, heads) row-major with Tsz = (2wd-1)(2wh-1)(2ww-1), indexed by
+ *   idx = ((dz+wd-1)*(2wh-1) + (dy+wh-1))*(2ww-1) + (dx+ww-1),  d* = query - key coords
+ *   (relative_position_index, swinfusion_module.py:93-103).  For kind 1 the caller passes
+ *   the already-activated 16*sigmoid(cpb_mlp(relative_coords_table)) (swin_v2_module.py:158-162).
+ * tau: kind 1 only, (heads) = exp(min(logit_scale, ln 100)) (swin_v2_module.py:154-156).
+ * Shift mask: -100 between tokens of different shift regions (swinfusion_module.py:317-338),
+ *   computed analytically from region ids, never materialised.
+ * out: rows with o_stride; lse: (B*D*H*W, heads) natural-log softmax normaliser per row. */
+int mmni_wattn_fwd(const mmni_wattn_desc* d,
+                   const float* q, const float* k, const float* v,
+                   const float* table, const float* tau,
+                   float* out, float* lse, void* stream);
+
+/* Backward (flash-style recompute from lse).  dq/dk/dv are fully overwritten (every token
+ * belongs to exactly one window).  dtable (Tsz, heads) and dtau (heads) are ACCUMULATED
+ * with atomics: the caller zeroes them.  dtau may be NULL for kind 0. */
+int mmni_wattn_bwd(const mmni_wattn_desc* d,
+                   const float* q, const float* k, const float* v,
+                   const float* table, const float* tau,
+                   const float* out, const float* dout, const float* lse,
+                   float* dq, float* dk, float* dv,
+                   float* dtable, float* dtau, void* stream);
+
+/* Integer maps the attention kernels use, exported for bit-exact parity tests (row a0).
+ *   mmni_window_rows:   rows[w*N + t] = source token row of window-local token t of window w
+ *                       (N = wd*wh*ww, w over all B*nW windows)
+ *   mmni_window_mask:   mask[w*N*N + i*N + j] in {0, -100} for the nW windows of ONE sample
+ *                       (calculate_mask, swinfusion_module.py:317-338)
+ *   mmni_relative_index: idx[i*N + j] (relative_position_index)                          */
+int mmni_window_rows(const mmni_wattn_desc* d, int32_t* rows, void* stream);
+int mmni_window_mask(const mmni_wattn_desc* d, float* mask, void* stream);
+int mmni_relative_index(const mmni_wattn_desc* d, int32_t* idx, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Crossmodal multi-head attention core:
+ *   modules/multihead_attention.py:51-134 between in_proj and out_proj:
+ *   softmax_fp32(q*scale @ k^T + mask) @ v, mask = -inf where (j - i) >= causal_diag
+ *   (buffered_future_mask, crossmodal_transformer.py:179-186, causal_diag = 1+|Tk-Tq|).
+ * Time-major layout (T, B, E): element (t, b, h, c) at ptr[(t*B + b)*stride + h*head_dim + c].
+ * ------------------------------------------------------------------------------------ */
+typedef struct mmni_mha_desc {
+    int32_t Tq, Tk, B, heads, head_dim;
+    int32_t causal_diag;        /* <= 0: no mask                                          */
+    float   scale;              /* head_dim^-0.5 (multihead_attention.py:22)              */
+    int64_t q_stride, k_stride, v_stride, o_stride;
+} mmni_mha_desc;
+
+/* out: (Tq, B, E) rows with o_stride; lse: (B, heads, Tq). */
+int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
+                 float* out, float* lse, void* stream);
+/* dq/dk/dv overwritten; workspace: (B, heads, Tq) floats for delta = rowsum(dO*O). */
+int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
+                 const float* out, const float* dout, const float* lse,
+                 float* dq, float* dk, float* dv, float* workspace, void* stream);
+/* Head-averaged attention probabilities (B, Tq, Tk) — the second return value of
+ * MultiheadAttention.forward (multihead_attention.py:131-133). */
+int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const float* k,
+                        const float* lse, float* probs, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * 3D convolutions.  Channels-last activations (B, D, H, W, C).
+ * Weights in PyTorch layout (Cout, Cin, kd, kh, kw); 2D convs pass kd = 1 on D = 1 volumes.
+ * ------------------------------------------------------------------------------------ */
+typedef struct mmni_conv3d_desc {
+    int32_t B, D, H, W, Cin;    /* input (2D reference convs use D = 1, kd = 1, pd = 0)      */
+    int32_t Cout;
+    int32_t kd, kh, kw;         /* kernel extents                                         */
+    int32_t sd, sh, sw;         /* strides: k==stride, pad 0 = patch-embed (swin_v2_module.py:483) */
+    int32_t pd, ph, pw;         /* zero padding: k3 s1 p1 = GreenBlock conv (nvidia_blocks.py:43) */
+    int32_t Do, Ho, Wo;         /* output extents                                         */
+    float   slope;              /* fused LeakyReLU negative slope; 1.0 = identity         */
+} mmni_conv3d_desc;
+
+/* Input is read as (B, D, H, W, Cin) channels-last; output written (B, Do, Ho, Wo, Cout). */
+int mmni_conv3d_fwd(const mmni_conv3d_desc* d, const float* x, const float* w,
+                    const float* bias, float* y, void* stream);
+/* dx overwritten (may be NULL); dw (Cout*Cin*kd*kh*kw) and db (Cout) ACCUMULATED (caller zeroes).
+ * y is the forward output, needed when slope != 1 to gate the LeakyReLU gradient. */
+int mmni_conv3d_bwd(const mmni_conv3d_desc* d, const float* x, const float* w,
+                    const float* y, const float* dy, float* dx, float* dw, float* db,
+                    void* stream);
+
+int mmni_version(void);
+const char* mmni_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMNI_H */

@@ -1,0 +1,351 @@
+// Channels-last 3D convolutions for gfx950.
+//
+//   a4  PatchEmbed conv, kernel == stride, pad 0   modules/swin_v2_module.py:483,496
+//       (3D lift: Conv3d(in, embed, k=s=patch))
+//   a4b Conv k3 s1 p1 + LeakyReLU(0.2)             model.py:1195-1198,1331,1366-1368 in the
+//       3D semantics of GreenBlock's Conv3d        nvidia_blocks.py:43,47
+//
+// Activations stay channels-last (B, D, H, W, C) — the token layout every Swin block uses —
+// so the reference's patch_unembed / patch_embed transposes (swinfusion_module.py:971,1010)
+// disappear.  Weights keep PyTorch's (Cout, Cin, k, k, k) layout.
+//
+// fwd : one lane per output voxel, all Cout accumulators in registers; weights are read with
+//       wave-uniform addresses (scalar loads), input rows through L1/L2.  Bias and the
+//       LeakyReLU are fused into the epilogue.
+// dx  : one lane per input voxel (gather form of the transposed conv, no atomics).
+// dw  : output tiles staged in LDS with their input halo; each lane owns (tap, cin) pairs
+//       and all Cout accumulators; workgroups are persistent over tiles and flush their
+//       partial dW/db once with atomics.
+#include "mmni_common.h"
+
+namespace mmni {
+
+struct ConvArgs {
+    int B, D, H, W, Cin, Cout, kd, kh, kw, sd, sh, sw, pd, ph, pw, Do, Ho, Wo;
+    float slope;
+    const float* x;
+    const float* w;
+    const float* bias;
+    float* y;
+    const float* dy;
+    float* dx;
+    float* dw;
+    float* db;
+    // dw tiling
+    int TZ, TY, TX, HZ, HY, HX, ntz, nty, ntx, ntiles;
+};
+
+__device__ __forceinline__ float lrelu_grad(float yv, float slope) { return yv > 0.f ? 1.f : slope; }
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv3d_fwd_kernel(ConvArgs a) {
+    const int64_t nvox = (int64_t)a.B * a.Do * a.Ho * a.Wo;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nvox) return;
+    int64_t r = e;
+    const int xo = (int)(r % a.Wo); r /= a.Wo;
+    const int yo = (int)(r % a.Ho); r /= a.Ho;
+    const int zo = (int)(r % a.Do);
+    const int b = (int)(r / a.Do);
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = a.bias ? a.bias[co] : 0.f;
+    const int K3 = a.kd * a.kh * a.kw;
+    const int z0 = zo * a.sd - a.pd, y0 = yo * a.sh - a.ph, x0 = xo * a.sw - a.pw;
+    for (int tz = 0; tz < a.kd; ++tz) {
+        const int z = z0 + tz;
+        if (z < 0 || z >= a.D) continue;
+        for (int ty = 0; ty < a.kh; ++ty) {
+            const int y = y0 + ty;
+            if (y < 0 || y >= a.H) continue;
+            const float* xrow = a.x + (((int64_t)b * a.D + z) * a.H + y) * a.W * CIN;
+            for (int tx = 0; tx < a.kw; ++tx) {
+                const int xx = x0 + tx;
+                if (xx < 0 || xx >= a.W) continue;
+                const int t = (tz * a.kh + ty) * a.kw + tx;
+                float xv[CIN];
+#pragma unroll
+                for (int ci = 0; ci < CIN; ++ci) xv[ci] = xrow[(int64_t)xx * CIN + ci];
+#pragma unroll
+                for (int co = 0; co < COUT; ++co) {
+                    const float* wr = a.w + ((int64_t)co * CIN) * K3 + t;
+                    float sacc = acc[co];
+#pragma unroll
+                    for (int ci = 0; ci < CIN; ++ci) sacc = fmaf(xv[ci], wr[(int64_t)ci * K3], sacc);
+                    acc[co] = sacc;
+                }
+            }
+        }
+    }
+    float* yo_p = a.y + e * COUT;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+        const float v = acc[co];
+        yo_p[co] = v > 0.f ? v : v * a.slope;
+    }
+}
+
+// dx[v][ci] = sum_t sum_co dz[u(v,t)][co] * w[co][ci][t]
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv3d_dx_kernel(ConvArgs a) {
+    const int64_t nvox = (int64_t)a.B * a.D * a.H * a.W;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nvox) return;
+    int64_t r = e;
+    const int x = (int)(r % a.W); r /= a.W;
+    const int y = (int)(r % a.H); r /= a.H;
+    const int z = (int)(r % a.D);
+    const int b = (int)(r / a.D);
+    float acc[CIN];
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci) acc[ci] = 0.f;
+    const int K3 = a.kd * a.kh * a.kw;
+    for (int tz = 0; tz < a.kd; ++tz) {
+        const int nz = z + a.pd - tz;
+        if (nz < 0 || nz % a.sd) continue;
+        const int uz = nz / a.sd;
+        if (uz >= a.Do) continue;
+        for (int ty = 0; ty < a.kh; ++ty) {
+            const int ny = y + a.ph - ty;
+            if (ny < 0 || ny % a.sh) continue;
+            const int uy = ny / a.sh;
+            if (uy >= a.Ho) continue;
+            for (int tx = 0; tx < a.kw; ++tx) {
+                const int nx = x + a.pw - tx;
+                if (nx < 0 || nx % a.sw) continue;
+                const int ux = nx / a.sw;
+                if (ux >= a.Wo) continue;
+                const int64_t u = (((int64_t)b * a.Do + uz) * a.Ho + uy) * a.Wo + ux;
+                const int t = (tz * a.kh + ty) * a.kw + tx;
+                float g[COUT];
+#pragma unroll
+                for (int co = 0; co < COUT; ++co) {
+                    g[co] = a.dy[u * COUT + co];
+                    if (a.slope != 1.f) g[co] *= lrelu_grad(a.y[u * COUT + co], a.slope);
+                }
+#pragma unroll
+                for (int ci = 0; ci < CIN; ++ci) {
+                    float sacc = acc[ci];
+#pragma unroll
+                    for (int co = 0; co < COUT; ++co)
+                        sacc = fmaf(g[co], a.w[((int64_t)co * CIN + ci) * K3 + t], sacc);
+                    acc[ci] = sacc;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci) a.dx[e * CIN + ci] = acc[ci];
+}
+
+// dW[co][ci][t] += sum_u dz[u][co] * x[in(u,t)][ci];  db[co] += sum_u dz[u][co]
+template <int CIN, int COUT, int MAXP>
+__global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int K3 = a.kd * a.kh * a.kw;
+    const int npairs = K3 * CIN;
+    const int Tout = a.TZ * a.TY * a.TX;
+    const int Tin = a.HZ * a.HY * a.HX;
+    float* dz_s = smem;                       // [Tout][COUT]
+    float* x_s = dz_s + Tout * COUT;          // [Tin][CIN]
+    const int tid = threadIdx.x;
+    float acc[MAXP][COUT];
+    float dbacc[COUT];
+#pragma unroll
+    for (int m = 0; m < MAXP; ++m)
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[m][co] = 0.f;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) dbacc[co] = 0.f;
+    const int tiles_per_b = a.ntz * a.nty * a.ntx;
+
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        int rr = tile;
+        const int bx = rr % a.ntx; rr /= a.ntx;
+        const int by = rr % a.nty; rr /= a.nty;
+        const int bz = rr % a.ntz;
+        const int b = rr / a.ntz;
+        (void)tiles_per_b;
+        const int oz0 = bz * a.TZ, oy0 = by * a.TY, ox0 = bx * a.TX;
+        const int iz0 = oz0 * a.sd - a.pd, iy0 = oy0 * a.sh - a.ph, ix0 = ox0 * a.sw - a.pw;
+        __syncthreads();
+        for (int e = tid; e < Tout; e += blockDim.x) {
+            const int lx = e % a.TX, ly = (e / a.TX) % a.TY, lz = e / (a.TX * a.TY);
+            const int oz = oz0 + lz, oy = oy0 + ly, ox = ox0 + lx;
+            float g[COUT];
+            if (oz < a.Do && oy < a.Ho && ox < a.Wo) {
+                const int64_t u = (((int64_t)b * a.Do + oz) * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+                for (int co = 0; co < COUT; ++co) {
+                    g[co] = a.dy[u * COUT + co];
+                    if (a.slope != 1.f) g[co] *= lrelu_grad(a.y[u * COUT + co], a.slope);
+                }
+            } else {
+#pragma unroll
+                for (int co = 0; co < COUT; ++co) g[co] = 0.f;
+            }
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) dz_s[e * COUT + co] = g[co];
+        }
+        for (int e = tid; e < Tin * CIN; e += blockDim.x) {
+            const int ci = e % CIN, v = e / CIN;
+            const int lx = v % a.HX, ly = (v / a.HX) % a.HY, lz = v / (a.HX * a.HY);
+            const int z = iz0 + lz, y = iy0 + ly, x = ix0 + lx;
+            float xv = 0.f;
+            if (z >= 0 && z < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
+                xv = a.x[((((int64_t)b * a.D + z) * a.H + y) * a.W + x) * CIN + ci];
+            x_s[e] = xv;
+        }
+        __syncthreads();
+        // pair (t, ci) owned by this lane: p = tid + m*256
+        for (int u = 0; u < Tout; ++u) {
+            const int ux = u % a.TX, uy = (u / a.TX) % a.TY, uz = u / (a.TX * a.TY);
+            float g[COUT];
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) g[co] = dz_s[u * COUT + co];
+            if (tid < COUT) {
+#pragma unroll
+                for (int co = 0; co < COUT; ++co)
+                    if (co == tid) dbacc[co] += g[co];
+            }
+#pragma unroll
+            for (int m = 0; m < MAXP; ++m) {
+                const int p = tid + m * 256;
+                if (p < npairs) {
+                    const int ci = p % CIN, t = p / CIN;
+                    const int tx = t % a.kw, ty = (t / a.kw) % a.kh, tz = t / (a.kw * a.kh);
+                    const int hv = ((uz * a.sd + tz) * a.HY + (uy * a.sh + ty)) * a.HX + (ux * a.sw + tx);
+                    const float xv = x_s[hv * CIN + ci];
+#pragma unroll
+                    for (int co = 0; co < COUT; ++co) acc[m][co] = fmaf(g[co], xv, acc[m][co]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < MAXP; ++m) {
+        const int p = tid + m * 256;
+        if (p < npairs) {
+            const int ci = p % CIN, t = p / CIN;
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) atomicAdd(&a.dw[((int64_t)co * CIN + ci) * K3 + t], acc[m][co]);
+        }
+    }
+    if (a.db && tid < COUT) {
+#pragma unroll
+        for (int co = 0; co < COUT; ++co)
+            if (co == tid) atomicAdd(&a.db[co], dbacc[co]);
+    }
+}
+
+static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
+    MMNI_ARG_CHECK(d != nullptr, "conv3d: null descriptor");
+    MMNI_ARG_CHECK(d->B > 0 && d->D > 0 && d->H > 0 && d->W > 0 && d->Cin > 0 && d->Cout > 0, "conv3d: bad sizes");
+    MMNI_ARG_CHECK(d->kd > 0 && d->kh > 0 && d->kw > 0 && d->sd > 0 && d->sh > 0 && d->sw > 0 && d->pd >= 0 &&
+                       d->ph >= 0 && d->pw >= 0,
+                   "conv3d: bad kernel/stride/pad");
+    auto osz = [](int n, int k, int s, int p) { return (n + 2 * p - k) / s + 1; };
+    MMNI_ARG_CHECK(d->Do == osz(d->D, d->kd, d->sd, d->pd) && d->Ho == osz(d->H, d->kh, d->sh, d->ph) &&
+                       d->Wo == osz(d->W, d->kw, d->sw, d->pw) && d->Do > 0 && d->Ho > 0 && d->Wo > 0,
+                   "conv3d: output extents (%d,%d,%d) inconsistent with input/kernel", d->Do, d->Ho, d->Wo);
+    a.B = d->B; a.D = d->D; a.H = d->H; a.W = d->W; a.Cin = d->Cin; a.Cout = d->Cout;
+    a.kd = d->kd; a.kh = d->kh; a.kw = d->kw; a.sd = d->sd; a.sh = d->sh; a.sw = d->sw;
+    a.pd = d->pd; a.ph = d->ph; a.pw = d->pw;
+    a.Do = d->Do; a.Ho = d->Ho; a.Wo = d->Wo;
+    a.slope = d->slope;
+    return 0;
+}
+
+template <int CIN, int COUT>
+static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
+    const int64_t n = (int64_t)a.B * a.Do * a.Ho * a.Wo;
+    conv3d_fwd_kernel<CIN, COUT><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
+    return launch_status("conv3d_fwd");
+}
+
+template <int CIN, int COUT>
+static int conv_bwd_launch(ConvArgs& a, hipStream_t s) {
+    if (a.dx) {
+        const int64_t n = (int64_t)a.B * a.D * a.H * a.W;
+        conv3d_dx_kernel<CIN, COUT><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
+        int rc = launch_status("conv3d_dx");
+        if (rc) return rc;
+    }
+    // dw tile: shrink until the LDS image (dz tile + input halo) fits 64 KiB
+    int TZ = 4, TY = 4, TX = 16;
+    auto hz = [&](int T) { return (T - 1) * a.sd + a.kd; };
+    auto hy = [&](int T) { return (T - 1) * a.sh + a.kh; };
+    auto hx = [&](int T) { return (T - 1) * a.sw + a.kw; };
+    if (a.Do == 1) TZ = 1;
+    auto bytes = [&]() {
+        return (size_t)(TZ * TY * TX * COUT + hz(TZ) * hy(TY) * hx(TX) * CIN) * 4;
+    };
+    while (bytes() > 64 * 1024) {
+        if (TX > 4) TX /= 2;
+        else if (TY > 1) TY /= 2;
+        else if (TZ > 1) TZ /= 2;
+        else if (TX > 1) TX /= 2;
+        else break;
+    }
+    MMNI_ARG_CHECK(bytes() <= 64 * 1024, "conv3d_dw: kernel too large for the LDS tile");
+    a.TZ = TZ; a.TY = TY; a.TX = TX;
+    a.HZ = hz(TZ); a.HY = hy(TY); a.HX = hx(TX);
+    a.ntz = (a.Do + TZ - 1) / TZ; a.nty = (a.Ho + TY - 1) / TY; a.ntx = (a.Wo + TX - 1) / TX;
+    a.ntiles = a.B * a.ntz * a.nty * a.ntx;
+    const int npairs = a.kd * a.kh * a.kw * CIN;
+    int grid = a.ntiles < kNumCU * 4 ? a.ntiles : kNumCU * 4;
+    const size_t lds = bytes();
+#define MMNI_DW(MP)                                                                            \
+    conv3d_dw_kernel<CIN, COUT, MP><<<grid, 256, lds, s>>>(a);                                 \
+    return launch_status("conv3d_dw");
+    if (npairs <= 256) { MMNI_DW(1) }
+    if (npairs <= 512) { MMNI_DW(2) }
+    if (npairs <= 768) { MMNI_DW(3) }
+    if (npairs <= 1024) { MMNI_DW(4) }
+#undef MMNI_DW
+    set_error("conv3d_dw: k^3*Cin = %d exceeds 1024 pairs", npairs);
+    return -2;
+}
+
+#define MMNI_CONV_DISPATCH(FN)                                                               \
+    {                                                                                        \
+        const int ci = a.Cin, co = a.Cout;                                                  \
+        hipStream_t st = (hipStream_t)stream;                                                \
+        if (ci == 1 && co == 12) return FN<1, 12>(a, st);                                    \
+        if (ci == 1 && co == 6) return FN<1, 6>(a, st);                                      \
+        if (ci == 6 && co == 12) return FN<6, 12>(a, st);                                    \
+        if (ci == 6 && co == 6) return FN<6, 6>(a, st);                                      \
+        if (ci == 24 && co == 12) return FN<24, 12>(a, st);                                  \
+        if (ci == 12 && co == 12) return FN<12, 12>(a, st);                                  \
+        if (ci == 12 && co == 6) return FN<12, 6>(a, st);                                    \
+        if (ci == 6 && co == 3) return FN<6, 3>(a, st);                                      \
+        if (ci == 3 && co == 1) return FN<3, 1>(a, st);                                      \
+        if (ci == 2 && co == 4) return FN<2, 4>(a, st);                                      \
+        set_error("conv3d: unsupported (Cin=%d, Cout=%d)", ci, co);                          \
+        return -2;                                                                           \
+    }
+
+}  // namespace mmni
+
+using namespace mmni;
+
+extern "C" int mmni_conv3d_fwd(const mmni_conv3d_desc* d, const float* x, const float* w, const float* bias,
+                               float* y, void* stream) {
+    ConvArgs a{};
+    int rc = conv_fill(d, a);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(x && w && y, "conv3d_fwd: null pointer");
+    a.x = x; a.w = w; a.bias = bias; a.y = y;
+    MMNI_CONV_DISPATCH(conv_fwd_launch)
+}
+
+extern "C" int mmni_conv3d_bwd(const mmni_conv3d_desc* d, const float* x, const float* w, const float* y,
+                               const float* dy, float* dx, float* dw, float* db, void* stream) {
+    ConvArgs a{};
+    int rc = conv_fill(d, a);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(x && w && dy && dw, "conv3d_bwd: null pointer");
+    MMNI_ARG_CHECK(d->slope == 1.f || y != nullptr, "conv3d_bwd: LeakyReLU gradient needs y");
+    a.x = x; a.w = w; a.y = const_cast<float*>(y); a.dy = dy; a.dx = dx; a.dw = dw; a.db = db;
+    MMNI_CONV_DISPATCH(conv_bwd_launch)
+}

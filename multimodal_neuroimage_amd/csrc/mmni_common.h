@@ -1,0 +1,40 @@
+// Internal helpers shared by the libmmni.so translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdint.h>
+#include "../../include/mmni.h"
+
+namespace mmni {
+
+// Thread-local last-error message behind mmni_last_error().
+void set_error(const char* fmt, ...);
+
+#define MMNI_ARG_CHECK(cond, ...)                 \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::mmni::set_error(__VA_ARGS__);       \
+            return -1;                            \
+        }                                         \
+    } while (0)
+
+inline int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+
+// Number of resident 64-lane waves a launch should aim for: 256 CUs x occupancy.
+constexpr int kNumCU = 256;
+
+}  // namespace mmni

@@ -1,0 +1,819 @@
+// Shifted-window attention for gfx950.
+//
+// Replaces, on the device:
+//   torch.roll + window_partition            modules/swin_v2_module.py:35-46,277-284
+//                                            modules/swinfusion_module.py:33-45,350-357
+//   WindowAttention_fusion.forward           modules/swinfusion_module.py:114-145
+//   Cross_WindowAttention.forward            modules/swinfusion_module.py:213-246
+//   WindowAttention.forward (cosine, Swin-V2) modules/swin_v2_module.py:138-178
+//   window_reverse + reverse roll            modules/swinfusion_module.py:366-373
+// between the qkv projection and the output projection (both stay GEMMs).
+//
+// Design (MI355X-first):
+//  * head_dim is 2 (SwinFusion) or 4 (Swin-V2): the QK^T and AV contractions have K = 2..4,
+//    far below any MFMA K-tile, so the kernels run the contractions on the fp32 VALU and
+//    account for that honestly in the roofline.
+//  * One workgroup owns WPB whole windows at a time (grid-stride over window groups, so the
+//    bias table is staged into LDS once per workgroup).  K/V of the window are gathered from
+//    the un-partitioned channels-last tensor straight into LDS: the roll/partition copies of
+//    the reference never exist in HBM.
+//  * Each query row is owned by KS adjacent lanes that split the keys; every lane keeps all
+//    heads of its row in registers so the relative index, shift-mask test and K/V broadcast
+//    reads are shared by all heads.  Partial softmax states merge with __shfl_xor.
+//  * Softmax runs in the log2 domain (q, bias and mask pre-scaled by log2 e) with an online
+//    max over chunks of CH keys: one v_exp_f32 per (row, key, head) + one per chunk.
+//  * The shift mask (-100 between regions) is the analytic region-equivalence rule, the
+//    relative-position index is code(query) - code(key) + offset — no N x N tensors in HBM.
+//  * Backward recomputes P from the saved log-sum-exp: pass A (lane = query row) produces
+//    dq and the bias-table gradient (LDS atomics, flushed once per workgroup), pass B
+//    (lane = key row) produces dk and dv.  dq/dk/dv need no cross-window reduction.
+#include "mmni_common.h"
+
+namespace mmni {
+
+struct WGeom {
+    int B, D, H, W;
+    int wd, wh, ww, sd, sh, sw;
+    int nWd, nWh, nWw;
+    int nwin;   // B * nWd * nWh * nWw
+    int N;      // tokens per window
+    int tw, th; // relative-code strides: (2wh-1)(2ww-1), (2ww-1)
+    int off;    // (wd-1)*tw + (wh-1)*th + (ww-1)
+    int Tsz;    // bias table rows
+};
+
+// Region id of a shifted-frame coordinate (swinfusion_module.py:321-331: slices
+// (0,-ws), (-ws,-s), (-s,None) filled with increasing ids).
+__device__ __host__ __forceinline__ int shift_region(int c, int L, int ws, int s) {
+    return s == 0 ? 0 : (c < L - ws ? 0 : (c < L - s ? 1 : 2));
+}
+
+struct TokenInfo {
+    int64_t row;  // source token row in the (B, D, H, W) tensor
+    int code;     // i*tw + j*th + k  (relative-position code)
+    int rc;       // packed per-axis region ids
+};
+
+__device__ __forceinline__ TokenInfo token_info(const WGeom& g, int w, int t) {
+    int r = w;
+    const int wx = r % g.nWw; r /= g.nWw;
+    const int wy = r % g.nWh; r /= g.nWh;
+    const int wz = r % g.nWd;
+    const int b = r / g.nWd;
+    const int k = t % g.ww;
+    const int r2 = t / g.ww;
+    const int j = r2 % g.wh;
+    const int i = r2 / g.wh;
+    const int cz = wz * g.wd + i, cy = wy * g.wh + j, cx = wx * g.ww + k;
+    int z = cz + g.sd; if (z >= g.D) z -= g.D;
+    int y = cy + g.sh; if (y >= g.H) y -= g.H;
+    int x = cx + g.sw; if (x >= g.W) x -= g.W;
+    TokenInfo ti;
+    ti.row = ((int64_t)(b * g.D + z) * g.H + y) * g.W + x;
+    ti.code = i * g.tw + j * g.th + k;
+    ti.rc = (shift_region(cz, g.D, g.wd, g.sd) * 3 + shift_region(cy, g.H, g.wh, g.sh)) * 3 +
+            shift_region(cx, g.W, g.ww, g.sw);
+    return ti;
+}
+
+struct WAArgs {
+    WGeom g;
+    int KS, WPB, NPAD, ngroups, kind;
+    float scale;
+    int64_t qs, ks, vs, os;
+    const float* q;
+    const float* k;
+    const float* v;
+    const float* table;
+    const float* tau;
+    float* out;
+    float* lse;
+    // backward
+    const float* o;
+    const float* dout;
+    float* dq;
+    float* dk;
+    float* dv;
+    float* dtable;
+    float* dtau;
+};
+
+constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
+constexpr float kNormEps = 1e-12f;          // F.normalize eps (swin_v2_module.py:153)
+constexpr int CH = 4;                       // keys per online-softmax chunk
+
+template <int C>
+__device__ __forceinline__ void load_row(float (&dst)[C], const float* src) {
+    if constexpr (C % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < C; c += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(src + c);
+            dst[c] = t.x; dst[c + 1] = t.y; dst[c + 2] = t.z; dst[c + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dst[c] = src[c];
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void store_row(float* dst, const float (&src)[C]) {
+    if constexpr (C % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < C; c += 4)
+            *reinterpret_cast<float4*>(dst + c) = make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dst[c] = src[c];
+    }
+}
+
+// Per-head L2 normalisation (F.normalize(dim=-1), eps 1e-12); returns the raw norms.
+template <int C, int HD>
+__device__ __forceinline__ void normalize_heads(float (&x)[C], float (&nrm)[C / HD]) {
+#pragma unroll
+    for (int h = 0; h < C / HD; ++h) {
+        float ss = 0.f;
+#pragma unroll
+        for (int c = 0; c < HD; ++c) ss += x[h * HD + c] * x[h * HD + c];
+        nrm[h] = sqrtf(ss);
+        const float inv = 1.0f / fmaxf(nrm[h], kNormEps);
+#pragma unroll
+        for (int c = 0; c < HD; ++c) x[h * HD + c] *= inv;
+    }
+}
+
+// Backward of y = x / max(||x||, eps) for one head: dx from dy, y and the raw norm.
+template <int HD>
+__device__ __forceinline__ void normalize_bwd(float* dx, const float* dy, const float* y, float nrm) {
+    if (nrm >= kNormEps) {
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < HD; ++c) dot += y[c] * dy[c];
+        const float inv = 1.0f / nrm;
+#pragma unroll
+        for (int c = 0; c < HD; ++c) dx[c] = (dy[c] - y[c] * dot) * inv;
+    } else {
+#pragma unroll
+        for (int c = 0; c < HD; ++c) dx[c] = dy[c] * (1.0f / kNormEps);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------
+template <int C, int HD, int KIND, int MAXT>
+__global__ __launch_bounds__(MAXT) void wattn_fwd_kernel(WAArgs a) {
+    constexpr int NH = C / HD;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB;
+    float* kv_s = smem;                                              // [WPB*NPAD][2C]
+    int2* meta_s = reinterpret_cast<int2*>(kv_s + (size_t)WPB * NPAD * 2 * C);  // [WPB*NPAD]
+    float* tab_s = reinterpret_cast<float*>(meta_s + WPB * NPAD);     // [Tsz][NH]
+
+    const int tid = threadIdx.x;
+    const int r = tid / KS, p = tid - r * KS;
+    const int wl = r / N, t = r - wl * N;
+    const int wl_c = wl < WPB ? wl : WPB - 1;
+
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+
+    float tau2[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) tau2[h] = (KIND == 1) ? a.tau[h] * kLog2e : a.scale * kLog2e;
+
+    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+        // ---- stage K/V of WPB windows (gathered through the shift) into LDS
+        for (int e = tid; e < WPB * NPAD; e += blockDim.x) {
+            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+            const int w = grp * WPB + w2;
+            float kr[C], vr[C];
+            int2 mt;
+            if (t2 < N && w < g.nwin) {
+                const TokenInfo ti = token_info(g, w, t2);
+                load_row<C>(kr, a.k + ti.row * a.ks);
+                load_row<C>(vr, a.v + ti.row * a.vs);
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
+                mt = make_int2(ti.code | (ti.rc << 16), 0);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) { kr[c] = 0.f; vr[c] = 0.f; }
+                mt = make_int2(0, __float_as_int(-INFINITY));
+            }
+            store_row<C>(kv_s + (size_t)e * 2 * C, kr);
+            store_row<C>(kv_s + (size_t)e * 2 * C + C, vr);
+            meta_s[e] = mt;
+        }
+
+        // ---- own query row (prescaled into the log2 domain)
+        const int w = grp * WPB + wl;
+        const bool active = (wl < WPB) && (w < g.nwin);
+        float q[C];
+        int cq = 0, rq = 0;
+        int64_t row = 0;
+        if (active) {
+            const TokenInfo ti = token_info(g, w, t);
+            row = ti.row;
+            cq = ti.code + g.off;
+            rq = ti.rc;
+            load_row<C>(q, a.q + row * a.qs);
+            if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(q, nrm); }
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) q[c] = 0.f;
+        }
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int c = 0; c < HD; ++c) q[h * HD + c] *= tau2[h];
+        __syncthreads();
+
+        float m[NH], l[NH], acc[C];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) { m[h] = -INFINITY; l[h] = 0.f; }
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+
+        const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
+        const int2* mw = meta_s + wl_c * NPAD;
+        const int nk = NPAD / KS;
+        for (int n = 0; n < nk; n += CH) {
+            float s[CH][NH];
+#pragma unroll
+            for (int cc = 0; cc < CH; ++cc) {
+                const int j = p + KS * (n + cc);
+                const int2 mt = mw[j];
+                const int code = mt.x & 0xffff, rcj = mt.x >> 16;
+                const float madd = (rcj == rq ? 0.f : kMask2) + __int_as_float(mt.y);
+                const float* tb = tab_s + (cq - code) * NH;
+                float kr[C];
+                load_row<C>(kr, kvw + (size_t)j * 2 * C);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    float d = tb[h] + madd;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) d = fmaf(q[h * HD + c], kr[h * HD + c], d);
+                    s[cc][h] = d;
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                float cm = s[0][h];
+#pragma unroll
+                for (int cc = 1; cc < CH; ++cc) cm = fmaxf(cm, s[cc][h]);
+                const float mn = fmaxf(m[h], cm);
+                const float alpha = fast_exp2(m[h] - mn);
+                m[h] = mn;
+                l[h] *= alpha;
+#pragma unroll
+                for (int c = 0; c < HD; ++c) acc[h * HD + c] *= alpha;
+            }
+#pragma unroll
+            for (int cc = 0; cc < CH; ++cc) {
+                const int j = p + KS * (n + cc);
+                float vr[C];
+                load_row<C>(vr, kvw + (size_t)j * 2 * C + C);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const float pj = fast_exp2(s[cc][h] - m[h]);
+                    l[h] += pj;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) acc[h * HD + c] = fmaf(pj, vr[h * HD + c], acc[h * HD + c]);
+                }
+            }
+        }
+        // ---- merge the KS partial states of this row (adjacent lanes)
+        for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const float mo = __shfl_xor(m[h], o);
+                const float lo = __shfl_xor(l[h], o);
+                const float mn = fmaxf(m[h], mo);
+                const float fa = fast_exp2(m[h] - mn), fb = fast_exp2(mo - mn);
+                l[h] = l[h] * fa + lo * fb;
+#pragma unroll
+                for (int c = 0; c < HD; ++c) {
+                    const float ao = __shfl_xor(acc[h * HD + c], o);
+                    acc[h * HD + c] = acc[h * HD + c] * fa + ao * fb;
+                }
+                m[h] = mn;
+            }
+        }
+        if (active && p == 0) {
+            float o[C];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const float inv = 1.0f / l[h];
+#pragma unroll
+                for (int c = 0; c < HD; ++c) o[h * HD + c] = acc[h * HD + c] * inv;
+                a.lse[row * NH + h] = (m[h] + fast_log2(l[h])) * kLn2;
+            }
+            store_row<C>(a.out + row * a.os, o);
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------
+template <int C, int HD, int KIND, int MAXT>
+__global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
+    constexpr int NH = C / HD;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB;
+    const int T = WPB * NPAD;
+    float* qd_s = smem;                                  // [T][2C]  a2 = prescaled q, dO
+    float* kv_s = qd_s + (size_t)T * 2 * C;              // [T][2C]  k (k-hat for kind 1), v
+    float* rs_s = kv_s + (size_t)T * 2 * C;              // [T][2*NH] lse2, delta
+    int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)T * 2 * NH);  // [T]
+    float* tab_s = reinterpret_cast<float*>(meta_s + T); // [Tsz][NH] (log2 domain)
+    float* dtab_s = tab_s + g.Tsz * NH;                  // [Tsz][NH] natural-domain grad
+    float* dtau_s = dtab_s + g.Tsz * NH;                 // [NH]
+
+    const int tid = threadIdx.x;
+    const int r = tid / KS, p = tid - r * KS;
+    const int wl = r / N, t = r - wl * N;
+    const int wl_c = wl < WPB ? wl : WPB - 1;
+    const int lane = tid & 63;
+
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
+        tab_s[e] = a.table[e] * kLog2e;
+        dtab_s[e] = 0.f;
+    }
+    if (tid < NH) dtau_s[tid] = 0.f;
+
+    float dtr[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) dtr[h] = 0.f;
+
+    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+        // ---- stage the window group
+        for (int e = tid; e < T; e += blockDim.x) {
+            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+            const int w = grp * WPB + w2;
+            float x0[C], x1[C];
+            float* rs = rs_s + (size_t)e * 2 * NH;
+            if (t2 < N && w < g.nwin) {
+                const TokenInfo ti = token_info(g, w, t2);
+                // q -> a2
+                load_row<C>(x0, a.q + ti.row * a.qs);
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(x0, nrm); }
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const float t2 = (KIND == 1) ? a.tau[h] * kLog2e : a.scale * kLog2e;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) x0[h * HD + c] *= t2;
+                }
+                load_row<C>(x1, a.dout + ti.row * a.os);
+                store_row<C>(qd_s + (size_t)e * 2 * C, x0);
+                store_row<C>(qd_s + (size_t)e * 2 * C + C, x1);
+                // delta = rowsum(dO * O) per head
+                load_row<C>(x0, a.o + ti.row * a.os);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    float dd = 0.f;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) dd = fmaf(x0[h * HD + c], x1[h * HD + c], dd);
+                    rs[h] = a.lse[ti.row * NH + h] * kLog2e;
+                    rs[NH + h] = dd;
+                }
+                load_row<C>(x0, a.k + ti.row * a.ks);
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(x0, nrm); }
+                load_row<C>(x1, a.v + ti.row * a.vs);
+                store_row<C>(kv_s + (size_t)e * 2 * C, x0);
+                store_row<C>(kv_s + (size_t)e * 2 * C + C, x1);
+                meta_s[e] = make_int2(ti.code | (ti.rc << 16), 0);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) x0[c] = 0.f;
+                store_row<C>(qd_s + (size_t)e * 2 * C, x0);
+                store_row<C>(qd_s + (size_t)e * 2 * C + C, x0);
+                store_row<C>(kv_s + (size_t)e * 2 * C, x0);
+                store_row<C>(kv_s + (size_t)e * 2 * C + C, x0);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) { rs[h] = INFINITY; rs[NH + h] = 0.f; }
+                meta_s[e] = make_int2(0, __float_as_int(-INFINITY));
+            }
+        }
+        __syncthreads();
+
+        const int w = grp * WPB + wl;
+        const bool active = (wl < WPB) && (w < g.nwin);
+        const int own = wl_c * NPAD + (active ? t : 0);
+        const int2 mown = meta_s[own];
+        const int cown = mown.x & 0xffff, rown = mown.x >> 16;
+        const float* qdw = qd_s + (size_t)wl_c * NPAD * 2 * C;
+        const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
+        const float* rsw = rs_s + (size_t)wl_c * NPAD * 2 * NH;
+        const int2* mw = meta_s + wl_c * NPAD;
+        const int nk = NPAD / KS;
+
+        // ================= pass A: lane = query row -> dq, dtable, dtau
+        {
+            float aq[C], dO[C], lse2[NH], dl[NH], dqa[C];
+            load_row<C>(aq, qd_s + (size_t)own * 2 * C);
+            load_row<C>(dO, qd_s + (size_t)own * 2 * C + C);
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                lse2[h] = active ? rs_s[(size_t)own * 2 * NH + h] : INFINITY;
+                dl[h] = rs_s[(size_t)own * 2 * NH + NH + h];
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) dqa[c] = 0.f;
+            const int cq = cown + g.off;
+            for (int n = 0; n < nk; ++n) {
+                const int j = p + KS * n;
+                const int2 mt = mw[j];
+                const int code = mt.x & 0xffff, rcj = mt.x >> 16;
+                const float madd = (rcj == rown ? 0.f : kMask2) + __int_as_float(mt.y);
+                const int tix = (cq - code) * NH;
+                float kr[C], vr[C];
+                load_row<C>(kr, kvw + (size_t)j * 2 * C);
+                load_row<C>(vr, kvw + (size_t)j * 2 * C + C);
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    float dot = 0.f, dp = 0.f;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) {
+                        dot = fmaf(aq[h * HD + c], kr[h * HD + c], dot);
+                        dp = fmaf(dO[h * HD + c], vr[h * HD + c], dp);
+                    }
+                    const float pr = fast_exp2(dot + tab_s[tix + h] + madd - lse2[h]);
+                    const float ds = pr * (dp - dl[h]);
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) dqa[h * HD + c] = fmaf(ds, kr[h * HD + c], dqa[h * HD + c]);
+                    atomicAdd(&dtab_s[tix + h], ds);
+                    if constexpr (KIND == 1) dtr[h] = fmaf(ds, dot, dtr[h]);
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) dqa[c] += __shfl_xor(dqa[c], o);
+            }
+            if (active && p == 0) {
+                const TokenInfo ti = token_info(g, w, t);
+                float dq[C];
+                if (KIND == 1) {
+                    float qr[C], nrm[NH];
+                    load_row<C>(qr, a.q + ti.row * a.qs);
+                    normalize_heads<C, HD>(qr, nrm);
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        float dy[HD];
+#pragma unroll
+                        for (int c = 0; c < HD; ++c) dy[c] = dqa[h * HD + c] * a.tau[h];
+                        normalize_bwd<HD>(dq + h * HD, dy, qr + h * HD, nrm[h]);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) dq[c] = dqa[c] * a.scale;
+                }
+                store_row<C>(a.dq + ti.row * a.qs, dq);
+            }
+        }
+
+        // ================= pass B: lane = key row -> dk, dv
+        {
+            float kr[C], vr[C], dka[C], dva[C];
+            load_row<C>(kr, kv_s + (size_t)own * 2 * C);
+            load_row<C>(vr, kv_s + (size_t)own * 2 * C + C);
+#pragma unroll
+            for (int c = 0; c < C; ++c) { dka[c] = 0.f; dva[c] = 0.f; }
+            const int ck = cown - g.off;
+            for (int n = 0; n < nk; ++n) {
+                const int i = p + KS * n;
+                const int2 mt = mw[i];
+                const int code = mt.x & 0xffff, rci = mt.x >> 16;
+                const float madd = (rci == rown ? 0.f : kMask2) + __int_as_float(mt.y);
+                const int tix = (code - ck) * NH;
+                float aq[C], dO[C];
+                load_row<C>(aq, qdw + (size_t)i * 2 * C);
+                load_row<C>(dO, qdw + (size_t)i * 2 * C + C);
+                const float* rsi = rsw + (size_t)i * 2 * NH;
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    float dot = 0.f, dp = 0.f;
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) {
+                        dot = fmaf(aq[h * HD + c], kr[h * HD + c], dot);
+                        dp = fmaf(dO[h * HD + c], vr[h * HD + c], dp);
+                    }
+                    const float pr = fast_exp2(dot + tab_s[tix + h] + madd - rsi[h]);
+                    const float ds = pr * (dp - rsi[NH + h]);
+#pragma unroll
+                    for (int c = 0; c < HD; ++c) {
+                        dva[h * HD + c] = fmaf(pr, dO[h * HD + c], dva[h * HD + c]);
+                        dka[h * HD + c] = fmaf(ds, aq[h * HD + c], dka[h * HD + c]);
+                    }
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    dka[c] += __shfl_xor(dka[c], o);
+                    dva[c] += __shfl_xor(dva[c], o);
+                }
+            }
+            if (active && p == 0) {
+                const TokenInfo ti = token_info(g, w, t);
+                float dk[C];
+                if (KIND == 1) {
+                    float kraw[C], nrm[NH];
+                    load_row<C>(kraw, a.k + ti.row * a.ks);
+                    normalize_heads<C, HD>(kraw, nrm);
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        float dy[HD];
+#pragma unroll
+                        for (int c = 0; c < HD; ++c) dy[c] = dka[h * HD + c] * kLn2;
+                        normalize_bwd<HD>(dk + h * HD, dy, kraw + h * HD, nrm[h]);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) dk[c] = dka[c] * kLn2;
+                }
+                store_row<C>(a.dk + ti.row * a.ks, dk);
+                store_row<C>(a.dv + ti.row * a.vs, dva);
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- dtau: wave reduce then one LDS atomic per wave; flush LDS accumulators
+    if (KIND == 1) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            float v = dtr[h];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == 0) atomicAdd(&dtau_s[h], v);
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
+        const float v = dtab_s[e];
+        if (v != 0.f) atomicAdd(&a.dtable[e], v);
+    }
+    if (KIND == 1 && tid < NH) {
+        // dtau = sum ds * (q-hat . k-hat);  dot was taken against tau*log2e*q-hat
+        atomicAdd(&a.dtau[tid], dtau_s[tid] / (a.tau[tid] * kLog2e));
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// integer maps (exported for parity tests)
+// ------------------------------------------------------------------------------------
+__global__ void window_rows_kernel(WGeom g, int32_t* rows) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)g.nwin * g.N) return;
+    const int w = (int)(e / g.N), t = (int)(e % g.N);
+    rows[e] = (int32_t)token_info(g, w, t).row;
+}
+
+__global__ void window_mask_kernel(WGeom g, int nWs, float* mask) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t NN = (int64_t)g.N * g.N;
+    if (e >= (int64_t)nWs * NN) return;
+    const int w = (int)(e / NN);
+    const int ij = (int)(e % NN);
+    const int i = ij / g.N, j = ij % g.N;
+    const int ri = token_info(g, w, i).rc, rj = token_info(g, w, j).rc;
+    mask[e] = (ri == rj) ? 0.f : -100.f;
+}
+
+__global__ void relative_index_kernel(WGeom g, int32_t* idx) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= g.N * g.N) return;
+    const int i = e / g.N, j = e % g.N;
+    idx[e] = token_info(g, 0, i).code - token_info(g, 0, j).code + g.off;
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+static int make_geom(const mmni_wattn_desc* d, WGeom& g) {
+    MMNI_ARG_CHECK(d != nullptr, "wattn: null descriptor");
+    MMNI_ARG_CHECK(d->B > 0 && d->D > 0 && d->H > 0 && d->W > 0, "wattn: bad extents B=%d D=%d H=%d W=%d",
+                   d->B, d->D, d->H, d->W);
+    MMNI_ARG_CHECK(d->wd > 0 && d->wh > 0 && d->ww > 0, "wattn: bad window");
+    MMNI_ARG_CHECK(d->D % d->wd == 0 && d->H % d->wh == 0 && d->W % d->ww == 0,
+                   "wattn: extents (%d,%d,%d) not multiples of window (%d,%d,%d)", d->D, d->H, d->W,
+                   d->wd, d->wh, d->ww);
+    MMNI_ARG_CHECK(d->sd >= 0 && d->sd < d->wd && d->sh >= 0 && d->sh < d->wh && d->sw >= 0 && d->sw < d->ww,
+                   "wattn: shift must satisfy 0 <= shift < window");
+    g.B = d->B; g.D = d->D; g.H = d->H; g.W = d->W;
+    g.wd = d->wd; g.wh = d->wh; g.ww = d->ww;
+    g.sd = d->sd; g.sh = d->sh; g.sw = d->sw;
+    g.nWd = d->D / d->wd; g.nWh = d->H / d->wh; g.nWw = d->W / d->ww;
+    const int64_t nwin = (int64_t)d->B * g.nWd * g.nWh * g.nWw;
+    MMNI_ARG_CHECK(nwin < (1ll << 31), "wattn: too many windows");
+    MMNI_ARG_CHECK((int64_t)d->B * d->D * d->H * d->W < (1ll << 31), "wattn: too many tokens");
+    g.nwin = (int)nwin;
+    g.N = d->wd * d->wh * d->ww;
+    g.th = 2 * d->ww - 1;
+    g.tw = (2 * d->wh - 1) * g.th;
+    g.off = (d->wd - 1) * g.tw + (d->wh - 1) * g.th + (d->ww - 1);
+    g.Tsz = (2 * d->wd - 1) * g.tw;
+    MMNI_ARG_CHECK(g.Tsz <= 0xffff, "wattn: relative table too large (%d)", g.Tsz);
+    return 0;
+}
+
+template <int C, int HD, int MAXT>
+struct WAKernels {
+    static void* fwd(int kind) {
+        return kind ? reinterpret_cast<void*>(&wattn_fwd_kernel<C, HD, 1, MAXT>)
+                    : reinterpret_cast<void*>(&wattn_fwd_kernel<C, HD, 0, MAXT>);
+    }
+    static void* bwd(int kind) {
+        return kind ? reinterpret_cast<void*>(&wattn_bwd_kernel<C, HD, 1, MAXT>)
+                    : reinterpret_cast<void*>(&wattn_bwd_kernel<C, HD, 0, MAXT>);
+    }
+};
+
+struct WAConfig {
+    int KS, WPB, NPAD, threads, ngroups, grid;
+    size_t lds;
+};
+
+static size_t wattn_lds_bytes(bool bwd, int C, int NH, int WPB, int NPAD, int Tsz) {
+    const size_t T = (size_t)WPB * NPAD;
+    if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
+    return T * 4 * C * 4 + T * 2 * NH * 4 + T * 8 + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
+}
+
+static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, WAConfig& cfg) {
+    const int N = g.N;
+    int KS = N >= 128 ? 4 : (N >= 32 ? 2 : 1);
+    auto r64 = [](int x) { return (x + 63) / 64 * 64; };
+    while (KS > 1 && r64(N * KS) > maxt) KS >>= 1;
+    MMNI_ARG_CHECK(r64(N) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
+    const int target = maxt < 512 ? maxt : 512;
+    int WPB = target / (N * KS);
+    if (WPB < 1) WPB = 1;
+    const int NPAD = (N + KS * CH - 1) / (KS * CH) * (KS * CH);
+    while (WPB > 1 && wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
+    const size_t lds = wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz);
+    MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
+    cfg.KS = KS;
+    cfg.WPB = WPB;
+    cfg.NPAD = NPAD;
+    cfg.threads = r64(WPB * N * KS);
+    cfg.ngroups = (g.nwin + WPB - 1) / WPB;
+    int per_cu = (int)((160 * 1024) / lds);
+    const int by_threads = 2048 / cfg.threads;
+    if (by_threads < per_cu) per_cu = by_threads;
+    if (per_cu > 8) per_cu = 8;
+    if (per_cu < 1) per_cu = 1;
+    const int resident = kNumCU * per_cu;
+    // forward: a few groups per block amortise the table staging; backward: one flush
+    // of the table gradient per block, so stay at one resident wave of blocks.
+    const int cap = bwd ? resident : resident * 4;
+    cfg.grid = cfg.ngroups < cap ? cfg.ngroups : cap;
+    cfg.lds = lds;
+    return 0;
+}
+
+static int dispatch(const mmni_wattn_desc* d, int HD, void*& kf, void*& kb, int& maxt) {
+    const int C = d->C;
+#define MMNI_WA_CASE(CC, HH, MT)                         \
+    if (C == CC && HD == HH) {                           \
+        kf = WAKernels<CC, HH, MT>::fwd(d->kind);        \
+        kb = WAKernels<CC, HH, MT>::bwd(d->kind);        \
+        maxt = MT;                                       \
+        return 0;                                        \
+    }
+    MMNI_WA_CASE(12, 2, 1024)
+    MMNI_WA_CASE(12, 4, 1024)
+    MMNI_WA_CASE(24, 2, 512)
+    MMNI_WA_CASE(24, 4, 512)
+    MMNI_WA_CASE(48, 4, 256)
+    MMNI_WA_CASE(6, 2, 1024)
+#undef MMNI_WA_CASE
+    set_error("wattn: unsupported (C=%d, head_dim=%d); supported: (12,2) (12,4) (24,2) (24,4) (48,4) (6,2)", C, HD);
+    return -2;
+}
+
+static int fill_args(const mmni_wattn_desc* d, WAArgs& a, int& HD) {
+    int rc = make_geom(d, a.g);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(d->heads > 0 && d->C % d->heads == 0, "wattn: C=%d not divisible by heads=%d", d->C, d->heads);
+    MMNI_ARG_CHECK(d->kind == 0 || d->kind == 1, "wattn: kind must be 0 or 1");
+    MMNI_ARG_CHECK(d->q_stride >= d->C && d->k_stride >= d->C && d->v_stride >= d->C && d->o_stride >= d->C,
+                   "wattn: token strides must be >= C");
+    HD = d->C / d->heads;
+    a.kind = d->kind;
+    a.scale = d->scale;
+    a.qs = d->q_stride; a.ks = d->k_stride; a.vs = d->v_stride; a.os = d->o_stride;
+    return 0;
+}
+
+// Dynamic LDS above 64 KiB: raise the per-function limit once (host-side attribute, no sync).
+static int ensure_lds_attr(void* fn, size_t bytes) {
+    if (bytes <= 64 * 1024) return 0;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) { set_error("hipFuncSetAttribute: %s", hipGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+// float4 row access needs 16-byte aligned rows when C % 4 == 0; scalar access otherwise.
+static bool row_aligned(const void* p, int64_t stride, int C) {
+    if (C % 4 != 0) return reinterpret_cast<uintptr_t>(p) % 4 == 0;
+    return (reinterpret_cast<uintptr_t>(p) % 16 == 0) && (stride % 4 == 0);
+}
+
+}  // namespace mmni
+
+using namespace mmni;
+
+extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
+                              const float* table, const float* tau, float* out, float* lse, void* stream) {
+    WAArgs a{};
+    int HD = 0;
+    int rc = fill_args(d, a, HD);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(q && k && v && table && out && lse, "wattn_fwd: null pointer");
+    MMNI_ARG_CHECK(d->kind == 0 || tau != nullptr, "wattn_fwd: kind 1 needs tau");
+    MMNI_ARG_CHECK(row_aligned(q, d->q_stride, d->C) && row_aligned(k, d->k_stride, d->C) &&
+                       row_aligned(v, d->v_stride, d->C) && row_aligned(out, d->o_stride, d->C),
+                   "wattn_fwd: q/k/v/out must be 16-byte aligned with strides multiple of 4");
+    void *kf, *kb;
+    int maxt;
+    rc = dispatch(d, HD, kf, kb, maxt);
+    if (rc) return rc;
+    WAConfig cfg;
+    rc = plan(a.g, d->C, d->heads, maxt, false, cfg);
+    if (rc) return rc;
+    a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
+    a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
+    rc = ensure_lds_attr(kf, cfg.lds);
+    if (rc) return rc;
+    void* args[] = {&a};
+    hipError_t e = hipLaunchKernel(kf, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
+    if (e != hipSuccess) { set_error("wattn_fwd launch: %s", hipGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
+                              const float* table, const float* tau, const float* out, const float* dout,
+                              const float* lse, float* dq, float* dk, float* dv, float* dtable, float* dtau,
+                              void* stream) {
+    WAArgs a{};
+    int HD = 0;
+    int rc = fill_args(d, a, HD);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(q && k && v && table && out && dout && lse && dq && dk && dv && dtable, "wattn_bwd: null pointer");
+    MMNI_ARG_CHECK(d->kind == 0 || (tau != nullptr && dtau != nullptr), "wattn_bwd: kind 1 needs tau and dtau");
+    MMNI_ARG_CHECK(row_aligned(q, d->q_stride, d->C) && row_aligned(k, d->k_stride, d->C) &&
+                       row_aligned(v, d->v_stride, d->C) && row_aligned(out, d->o_stride, d->C) &&
+                       row_aligned(dout, d->o_stride, d->C) && row_aligned(dq, d->q_stride, d->C) &&
+                       row_aligned(dk, d->k_stride, d->C) && row_aligned(dv, d->v_stride, d->C),
+                   "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
+    void *kf, *kb;
+    int maxt;
+    rc = dispatch(d, HD, kf, kb, maxt);
+    if (rc) return rc;
+    WAConfig cfg;
+    rc = plan(a.g, d->C, d->heads, maxt, true, cfg);
+    if (rc) return rc;
+    a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
+    a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
+    a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;
+    rc = ensure_lds_attr(kb, cfg.lds);
+    if (rc) return rc;
+    void* args[] = {&a};
+    hipError_t e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
+    if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+extern "C" int mmni_window_rows(const mmni_wattn_desc* d, int32_t* rows, void* stream) {
+    WGeom g;
+    int rc = make_geom(d, g);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(rows != nullptr, "window_rows: null pointer");
+    const int64_t n = (int64_t)g.nwin * g.N;
+    window_rows_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(g, rows);
+    return launch_status("window_rows");
+}
+
+extern "C" int mmni_window_mask(const mmni_wattn_desc* d, float* mask, void* stream) {
+    WGeom g;
+    int rc = make_geom(d, g);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(mask != nullptr, "window_mask: null pointer");
+    const int nWs = g.nWd * g.nWh * g.nWw;
+    const int64_t n = (int64_t)nWs * g.N * g.N;
+    window_mask_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(g, nWs, mask);
+    return launch_status("window_mask");
+}
+
+extern "C" int mmni_relative_index(const mmni_wattn_desc* d, int32_t* idx, void* stream) {
+    WGeom g;
+    int rc = make_geom(d, g);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(idx != nullptr, "relative_index: null pointer");
+    relative_index_kernel<<<(g.N * g.N + 255) / 256, 256, 0, (hipStream_t)stream>>>(g, idx);
+    return launch_status("relative_index");
+}

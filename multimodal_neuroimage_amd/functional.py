@@ -1,0 +1,319 @@
+"""torch.autograd wrappers over the libmmni.so C ABI (include/mmni.h).
+
+Every op here runs the hand-written HIP kernels; there is no eager/CPU fallback: inputs that
+are not float32 ROCm-device tensors raise.  Outputs and saved tensors are allocated by torch
+(caching allocator), the library only launches on torch's current stream.
+"""
+from dataclasses import dataclass
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr, require_device, stream_handle
+
+LN100 = math.log(1.0 / 0.01)
+
+
+@dataclass(frozen=True)
+class WindowGeometry:
+    """Volume grid + window + cyclic shift of one shifted-window attention call.
+
+    2D reference shapes use D = 1, window (1, wh, ww), shift (0, sh, sw).
+    """
+    B: int
+    spatial: tuple       # (D, H, W)
+    window: tuple        # (wd, wh, ww)
+    shift: tuple         # (sd, sh, sw)
+
+    @property
+    def tokens(self):
+        D, H, W = self.spatial
+        return self.B * D * H * W
+
+    @property
+    def N(self):
+        wd, wh, ww = self.window
+        return wd * wh * ww
+
+    @property
+    def table_rows(self):
+        wd, wh, ww = self.window
+        return (2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1)
+
+    @staticmethod
+    def make(B, spatial, window, shift):
+        spatial = tuple(int(s) for s in spatial)
+        if len(spatial) == 2:
+            spatial = (1,) + spatial
+        if isinstance(window, int):
+            window = (window,) * 3 if len(spatial) == 3 and spatial[0] > 1 else (1, window, window)
+        window = tuple(int(w) for w in window)
+        if len(window) == 2:
+            window = (1,) + window
+        if isinstance(shift, int):
+            shift = tuple(shift if w > 1 else 0 for w in window)
+        shift = tuple(int(s) for s in shift)
+        if len(shift) == 2:
+            shift = (0,) + shift
+        return WindowGeometry(int(B), spatial, window, shift)
+
+
+def _wattn_desc(g, C, heads, kind, scale, qs, ks, vs, os_):
+    d = _lib.WAttnDesc()
+    d.B = g.B
+    d.D, d.H, d.W = g.spatial
+    d.C = C
+    d.heads = heads
+    d.wd, d.wh, d.ww = g.window
+    d.sd, d.sh, d.sw = g.shift
+    d.kind = kind
+    d.scale = float(scale)
+    d.q_stride, d.k_stride, d.v_stride, d.o_stride = int(qs), int(ks), int(vs), int(os_)
+    return d
+
+
+def _row_view(t, C, offset):
+    """(rows, stride) view of channels [offset, offset+C) of a (rows, stride) tensor."""
+    return t[:, offset:offset + C]
+
+
+class _WindowAttention(torch.autograd.Function):
+    """Fused shift + partition + window attention + reverse, on token rows.
+
+    q_src: (rows, Cq_total) with q in columns [0, C); kv_src: (rows, Ckv_total) with k in
+    [k_off, k_off+C) and v in [v_off, v_off+C).  For self attention q_src is kv_src (packed
+    qkv, offsets 0/C/2C).  Returns (rows, C).
+    """
+
+    @staticmethod
+    def forward(ctx, q_src, kv_src, table, tau, geom, heads, kind, scale, k_off, v_off, packed):
+        C = q_src.shape[1] // 3 if packed else q_src.shape[1]
+        require_device(q_src, kv_src, table, tau, what="window_attention")
+        rows = q_src.shape[0]
+        assert rows == geom.tokens, f"window_attention: {rows} rows != geometry tokens {geom.tokens}"
+        assert q_src.stride(1) == 1 and kv_src.stride(1) == 1
+        table = table.contiguous()
+        tau_c = tau.contiguous() if tau is not None else None
+        out = torch.empty((rows, C), device=q_src.device, dtype=torch.float32)
+        lse = torch.empty((rows, heads), device=q_src.device, dtype=torch.float32)
+        q = q_src
+        k = kv_src[:, k_off:]
+        v = kv_src[:, v_off:]
+        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
+        L = _lib.load()
+        check(L.mmni_wattn_fwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau_c), ptr(out), ptr(lse),
+                               stream_handle(q_src.device)), "mmni_wattn_fwd")
+        ctx.save_for_backward(q_src, kv_src, table, tau_c, out, lse)
+        ctx.cfg = (geom, heads, kind, scale, k_off, v_off, packed, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q_src, kv_src, table, tau, out, lse = ctx.saved_tensors
+        geom, heads, kind, scale, k_off, v_off, packed, C = ctx.cfg
+        dout = dout.contiguous()
+        if packed:
+            dq_src = torch.empty_like(q_src)
+            dkv_src = dq_src
+        else:
+            dq_src = torch.empty_like(q_src)
+            dkv_src = torch.empty_like(kv_src)
+            if kv_src.shape[1] > 2 * C or (k_off, v_off) != (0, C):
+                dkv_src.zero_()
+        dtable = torch.zeros_like(table)
+        dtau = torch.zeros_like(tau) if tau is not None else None
+        q, k, v = q_src, kv_src[:, k_off:], kv_src[:, v_off:]
+        dq, dk, dv = dq_src, dkv_src[:, k_off:], dkv_src[:, v_off:]
+        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
+        L = _lib.load()
+        check(L.mmni_wattn_bwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau), ptr(out), ptr(dout), ptr(lse),
+                               ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau),
+                               stream_handle(q_src.device)), "mmni_wattn_bwd")
+        if packed:
+            return dq_src, None, dtable, dtau, None, None, None, None, None, None, None
+        return dq_src, dkv_src, dtable, dtau, None, None, None, None, None, None, None
+
+
+def window_attention_self(qkv, table, geom, heads, *, kind=0, scale=None, tau=None):
+    """Self window attention on packed qkv token rows (rows, 3C) -> (rows, C)."""
+    C = qkv.shape[-1] // 3
+    qkv2 = qkv.reshape(-1, 3 * C)
+    if not qkv2.is_contiguous():
+        qkv2 = qkv2.contiguous()
+    if scale is None:
+        scale = (C // heads) ** -0.5
+    return _WindowAttention.apply(qkv2, qkv2, table, tau, geom, heads, kind, scale, C, 2 * C, True)
+
+
+def window_attention_cross(q, kv, table, geom, heads, *, kind=0, scale=None, tau=None):
+    """Cross window attention: q rows (rows, C) from x, kv rows (rows, 2C) from y."""
+    C = q.shape[-1]
+    q2 = q.reshape(-1, C).contiguous()
+    kv2 = kv.reshape(-1, 2 * C).contiguous()
+    if scale is None:
+        scale = (C // heads) ** -0.5
+    return _WindowAttention.apply(q2, kv2, table, tau, geom, heads, kind, scale, 0, C, False)
+
+
+def window_rows(geom, device):
+    """Integer gather map rows[w*N + t] used by the kernels (row a0)."""
+    n = geom.B * (geom.spatial[0] // geom.window[0]) * (geom.spatial[1] // geom.window[1]) * \
+        (geom.spatial[2] // geom.window[2]) * geom.N
+    out = torch.empty(n, dtype=torch.int32, device=device)
+    d = _wattn_desc(geom, 12, 6, 0, 1.0, 12, 12, 12, 12)
+    check(_lib.load().mmni_window_rows(d, ptr(out), stream_handle(device)), "mmni_window_rows")
+    return out
+
+
+def window_mask(geom, device):
+    """(nW, N, N) shift mask of one sample, {0, -100} (calculate_mask equivalent)."""
+    nW = (geom.spatial[0] // geom.window[0]) * (geom.spatial[1] // geom.window[1]) * \
+        (geom.spatial[2] // geom.window[2])
+    out = torch.empty((nW, geom.N, geom.N), dtype=torch.float32, device=device)
+    d = _wattn_desc(geom, 12, 6, 0, 1.0, 12, 12, 12, 12)
+    check(_lib.load().mmni_window_mask(d, ptr(out), stream_handle(device)), "mmni_window_mask")
+    return out
+
+
+def relative_index(geom, device):
+    out = torch.empty((geom.N, geom.N), dtype=torch.int32, device=device)
+    d = _wattn_desc(geom, 12, 6, 0, 1.0, 12, 12, 12, 12)
+    check(_lib.load().mmni_relative_index(d, ptr(out), stream_handle(device)), "mmni_relative_index")
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# crossmodal multi-head attention core
+# ----------------------------------------------------------------------------------------
+def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_):
+    d = _lib.MhaDesc()
+    d.Tq, d.Tk, d.B, d.heads, d.head_dim = Tq, Tk, B, heads, hd
+    d.causal_diag = int(causal_diag)
+    d.scale = float(scale)
+    d.q_stride, d.k_stride, d.v_stride, d.o_stride = int(qs), int(ks), int(vs), int(os_)
+    return d
+
+
+class _MHA(torch.autograd.Function):
+    """q (Tq, B, E), k/v (Tk, B, E) dense time-major tensors -> out (Tq, B, E), lse (B, h, Tq)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, heads, causal_diag, scale):
+        require_device(q, k, v, what="mha")
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        Tq, B, E = q.shape
+        Tk = k.shape[0]
+        out = torch.empty((Tq, B, E), device=q.device, dtype=torch.float32)
+        lse = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        check(_lib.load().mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse),
+                                        stream_handle(q.device)), "mmni_mha_fwd")
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.cfg = (heads, causal_diag, scale)
+        ctx.mark_non_differentiable(lse)
+        return out, lse
+
+    @staticmethod
+    def backward(ctx, dout, _dlse):
+        q, k, v, out, lse = ctx.saved_tensors
+        heads, causal_diag, scale = ctx.cfg
+        Tq, B, E = q.shape
+        Tk = k.shape[0]
+        dout = dout.contiguous()
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        dv = torch.empty_like(v)
+        ws = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        check(_lib.load().mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
+                                        ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
+              "mmni_mha_bwd")
+        return dq, dk, dv, None, None, None
+
+
+def mha_core(q, k, v, heads, causal_diag=0, scale=None):
+    """softmax(q*scale @ k^T + causal) @ v over (T, B, E) time-major tensors.
+
+    Returns (out, lse); lse (B, heads, Tq) feeds mha_mean_probs.
+    """
+    E = q.shape[-1]
+    if scale is None:
+        scale = (E // heads) ** -0.5
+    return _MHA.apply(q, k, v, heads, causal_diag, scale)
+
+
+def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None):
+    """Head-averaged attention weights (B, Tq, Tk) (multihead_attention.py:131-133)."""
+    Tq, B, E = q.shape
+    Tk = k.shape[0]
+    if scale is None:
+        scale = (E // heads) ** -0.5
+    q = q.detach()
+    k = k.detach()
+    if q.stride(1) != E or q.stride(0) != B * E:
+        q = q.contiguous()
+    if k.stride(1) != E or k.stride(0) != B * E:
+        k = k.contiguous()
+    probs = torch.empty((B, Tq, Tk), device=q.device, dtype=torch.float32)
+    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+    check(_lib.load().mmni_mha_mean_probs(d, ptr(q), ptr(k), ptr(lse), ptr(probs), stream_handle(q.device)),
+          "mmni_mha_mean_probs")
+    return probs
+
+
+# ----------------------------------------------------------------------------------------
+# channels-last 3D convolution
+# ----------------------------------------------------------------------------------------
+def _triple(v):
+    return tuple(int(a) for a in v) if isinstance(v, (tuple, list)) else (int(v),) * 3
+
+
+def _conv_desc(x_shape, w_shape, stride, pad, slope):
+    B, D, H, W, Cin = x_shape
+    Cout, _, kd, kh, kw = w_shape
+    sd, sh, sw = stride
+    pd, ph, pw = pad
+    d = _lib.Conv3dDesc()
+    d.B, d.D, d.H, d.W, d.Cin, d.Cout = B, D, H, W, Cin, Cout
+    d.kd, d.kh, d.kw, d.sd, d.sh, d.sw, d.pd, d.ph, d.pw = kd, kh, kw, sd, sh, sw, pd, ph, pw
+    d.Do = (D + 2 * pd - kd) // sd + 1
+    d.Ho = (H + 2 * ph - kh) // sh + 1
+    d.Wo = (W + 2 * pw - kw) // sw + 1
+    d.slope = float(slope)
+    return d
+
+
+class _Conv3d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, slope):
+        require_device(x, weight, bias, what="conv3d")
+        x = x.contiguous()
+        weight = weight.contiguous()
+        assert weight.dim() == 5 and x.dim() == 5 and x.shape[-1] == weight.shape[1]
+        d = _conv_desc(tuple(x.shape), tuple(weight.shape), stride, pad, slope)
+        y = torch.empty((d.B, d.Do, d.Ho, d.Wo, d.Cout), device=x.device, dtype=torch.float32)
+        check(_lib.load().mmni_conv3d_fwd(d, ptr(x), ptr(weight), ptr(bias), ptr(y), stream_handle(x.device)),
+              "mmni_conv3d_fwd")
+        ctx.save_for_backward(x, weight, y if slope != 1.0 else None)
+        ctx.cfg = (stride, pad, slope, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        stride, pad, slope, has_bias = ctx.cfg
+        dy = dy.contiguous()
+        d = _conv_desc(tuple(x.shape), tuple(weight.shape), stride, pad, slope)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.zeros_like(weight)
+        db = torch.zeros(d.Cout, device=x.device, dtype=torch.float32) if has_bias else None
+        check(_lib.load().mmni_conv3d_bwd(d, ptr(x), ptr(weight), ptr(y), ptr(dy), ptr(dx), ptr(dw), ptr(db),
+                                           stream_handle(x.device)), "mmni_conv3d_bwd")
+        return dx, dw, db, None, None, None
+
+
+def conv3d_cl(x, weight, bias=None, stride=1, pad=0, slope=1.0):
+    """Channels-last conv: x (B, D, H, W, Cin), weight (Cout, Cin, kd, kh, kw) ->
+    (B, Do, Ho, Wo, Cout) with a fused LeakyReLU(slope) (slope 1 = identity)."""
+    return _Conv3d.apply(x, weight, bias, _triple(stride), _triple(pad), slope)

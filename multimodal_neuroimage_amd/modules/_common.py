@@ -1,0 +1,115 @@
+"""Helpers shared by the window-attention modules (host side, torch).
+
+The buffers built here (relative_position_index, attn_mask, relative_coords_table) exist only so
+state_dicts keep the reference's keys and shapes; the HIP kernels compute the
+index and the mask analytically and never read them.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from ..functional import WindowGeometry
+
+
+def to_ntuple(x, n):
+    if isinstance(x, (list, tuple)):
+        return tuple(x)
+    return (x,) * n
+
+
+def to_2tuple(x):
+    return to_ntuple(x, 2)
+
+
+def trunc_normal_(t, std=1.0, mean=0.0, a=-2.0, b=2.0):
+    return nn.init.trunc_normal_(t, mean=mean, std=std, a=a, b=b)
+
+
+class DropPath(nn.Module):
+    """Per-sample stochastic depth (timm.models.layers.DropPath semantics)."""
+
+    def __init__(self, drop_prob=0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        if self.drop_prob == 0.0 or not self.training:
+            return x
+        keep = 1.0 - self.drop_prob
+        mask = x.new_empty((x.shape[0],) + (1,) * (x.ndim - 1)).bernoulli_(keep)
+        return x * mask / keep
+
+
+def relative_index_buffer(window):
+    """relative_position_index of a window (any number of axes), int64 (N, N)."""
+    axes = [torch.arange(w) for w in window]
+    coords = torch.stack(torch.meshgrid(*axes, indexing="ij")).flatten(1)
+    rel = coords[:, :, None] - coords[:, None, :]
+    idx = torch.zeros(rel.shape[1:], dtype=torch.long)
+    for a, w in enumerate(window):
+        idx = idx * (2 * w - 1) + rel[a] + (w - 1)
+    return idx
+
+
+def shift_mask_buffer(resolution, window, shift):
+    """(nW, N, N) {0, -100} mask of one sample for a shifted-window layer of `resolution`."""
+    nd = len(resolution)
+    label = torch.zeros(resolution, dtype=torch.long)
+    for a, (L, w, s) in enumerate(zip(resolution, window, shift)):
+        lab = torch.zeros(L, dtype=torch.long)
+        if s > 0:
+            lab[L - w:L - s] = 1
+            lab[L - s:] = 2
+        view = [1] * nd
+        view[a] = L
+        label = label * 3 + lab.view(view)
+    split = []
+    for L, w in zip(resolution, window):
+        split += [L // w, w]
+    perm = [2 * a for a in range(nd)] + [2 * a + 1 for a in range(nd)]
+    win = label.view(split).permute(perm).reshape(-1, math.prod(window))
+    diff = win.unsqueeze(1) - win.unsqueeze(2)
+    return torch.zeros(diff.shape).masked_fill(diff != 0, -100.0)
+
+
+def clamp_window(input_resolution, window_size, shift_size):
+    """Window/shift clamp of the Swin blocks (swin_v2_module.py:226-231,
+    swinfusion_module.py:294-298): a layer no larger than its window attends globally."""
+    if min(input_resolution) <= window_size:
+        return min(input_resolution), 0
+    return window_size, shift_size
+
+
+def geometry(batch, x_size, window_size, shift_size):
+    """WindowGeometry of a block applied at spatial size x_size (2D or 3D)."""
+    x_size = tuple(int(s) for s in x_size)
+    nd = len(x_size)
+    win = to_ntuple(window_size, nd)
+    sh = to_ntuple(shift_size, nd)
+    return WindowGeometry.make(batch, x_size, win if nd == 3 else (1,) + tuple(win),
+                               sh if nd == 3 else (0,) + tuple(sh))
+
+
+def patch_merge_gather(x, resolution):
+    """Concatenate the 2^k neighbours of a token grid (B, prod(res), C) -> (B, prod(res/2), 2^k C).
+
+    2D order is the reference's (h fastest): (0,0),(1,0),(0,1),(1,1) (swin_v2_module.py:354-358).
+    The 3D lift extends it with the first axis fastest: offsets (dz,dy,dx) enumerated with dz
+    varying fastest, then dy, then dx (so D = 1 reduces to the 2D order).
+    """
+    B, L, C = x.shape
+    nd = len(resolution)
+    x = x.view(B, *resolution, C)
+    parts = []
+    if nd == 2:
+        for dx in (0, 1):
+            for dy in (0, 1):
+                parts.append(x[:, dy::2, dx::2, :])
+    else:
+        for dx in (0, 1):
+            for dy in (0, 1):
+                for dz in (0, 1):
+                    parts.append(x[:, dz::2, dy::2, dx::2, :])
+    y = torch.cat(parts, -1)
+    return y.view(B, -1, (2 ** nd) * C)

@@ -1,0 +1,89 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol include/mmni.h
+declares, reports its version, and rejects bad descriptors with the documented error
+convention before any device work."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from multimodal_neuroimage_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "mmni.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mmni_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), f"libmmni.so lacks {s}"
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes bindings out of sync with include/mmni.h"
+
+
+def test_version():
+    assert _lib.load().mmni_version() == _lib.ABI_VERSION
+
+
+def _wdesc(**kw):
+    d = _lib.WAttnDesc()
+    base = dict(B=1, D=1, H=12, W=12, C=12, heads=6, wd=1, wh=6, ww=6, sd=0, sh=3, sw=3, kind=0, scale=0.7,
+                q_stride=36, k_stride=36, v_stride=36, o_stride=12)
+    base.update(kw)
+    for k, v in base.items():
+        setattr(d, k, v)
+    return d
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(H=13), "multiples of window"),
+    (dict(sh=6), "shift"),
+    (dict(C=10), "divisible"),
+    (dict(kind=3), "kind"),
+    (dict(q_stride=4), "strides"),
+])
+def test_wattn_rejects_bad_descriptors(bad, msg):
+    lib = _lib.load()
+    d = _wdesc(**bad)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None)
+    assert rc < 0
+    assert msg in lib.mmni_last_error().decode()
+
+
+def test_wattn_rejects_unsupported_head_dim():
+    lib = _lib.load()
+    d = _wdesc(C=20, heads=2, q_stride=60, k_stride=60, v_stride=60, o_stride=20)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None)
+    assert rc == -2
+    assert "unsupported" in lib.mmni_last_error().decode()
+
+
+def test_mha_and_conv_reject_bad_descriptors():
+    lib = _lib.load()
+    d = _lib.MhaDesc()
+    d.Tq, d.Tk, d.B, d.heads, d.head_dim, d.causal_diag, d.scale = 8, 8, 1, 2, 5, 0, 1.0
+    d.q_stride = d.k_stride = d.v_stride = d.o_stride = 10
+    p = ctypes.c_void_p(16)
+    assert lib.mmni_mha_fwd(d, p, p, p, p, p, None) == -2
+    c = _lib.Conv3dDesc()
+    for k, v in dict(B=1, D=8, H=8, W=8, Cin=1, Cout=12, kd=4, kh=4, kw=4, sd=4, sh=4, sw=4, pd=0, ph=0, pw=0,
+                     Do=3, Ho=2, Wo=2, slope=1.0).items():
+        setattr(c, k, v)
+    assert lib.mmni_conv3d_fwd(c, p, p, None, p, None) < 0
+    assert "inconsistent" in lib.mmni_last_error().decode()
+
+
+def test_product_path_has_no_cpu_fallback():
+    from multimodal_neuroimage_amd.functional import window_attention_self, WindowGeometry
+    geom = WindowGeometry.make(1, (12, 12), (1, 6, 6), (0, 0, 0))
+    qkv = torch.zeros(144, 36)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        window_attention_self(qkv, torch.zeros(121, 6), geom, 6)

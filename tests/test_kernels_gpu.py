@@ -1,0 +1,199 @@
+"""HIP kernels (through the C ABI) vs the oracle, on seeded random inputs, 2D and 3D.
+
+Integer maps: bit-exact.  Float kernels (fp32) vs the float64 oracle: max error relative to the
+reference's max magnitude <= 1e-4 (the north-star bar is 1e-3 rel in fp32)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as O
+from oracle.index_maps import shifted_window_rows, shift_mask, relative_position_index
+from multimodal_neuroimage_amd import functional as MF
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-6))
+
+
+GEOMS = [
+    (2, (1, 12, 18), (1, 6, 6), (0, 3, 3)),
+    (2, (1, 84, 84), (1, 6, 6), (0, 3, 3)),
+    (2, (1, 6, 6), (1, 3, 3), (0, 1, 1)),
+    (1, (12, 12, 12), (6, 6, 6), (3, 3, 3)),
+    (2, (6, 12, 18), (3, 6, 6), (1, 3, 3)),
+    (1, (12, 12, 12), (6, 6, 6), (0, 0, 0)),
+]
+
+
+@pytest.mark.parametrize("B,spatial,window,shift", GEOMS)
+def test_window_maps_bit_exact(device, B, spatial, window, shift):
+    g = MF.WindowGeometry(B, spatial, window, shift)
+    rows = MF.window_rows(g, device).cpu().numpy().reshape(-1, g.N)
+    np.testing.assert_array_equal(rows, shifted_window_rows(B, spatial, window, shift))
+    mask = MF.window_mask(g, device).cpu().numpy()
+    if any(shift):
+        np.testing.assert_array_equal(mask, shift_mask(spatial, window, shift))
+    else:
+        assert (mask == 0).all()
+    idx = MF.relative_index(g, device).cpu().numpy()
+    np.testing.assert_array_equal(idx, relative_position_index(window))
+
+
+def test_window_maps_full_volume_96(device):
+    g = MF.WindowGeometry(1, (96, 96, 96), (6, 6, 6), (3, 3, 3))
+    rows = MF.window_rows(g, device).cpu().numpy().reshape(-1, g.N)
+    np.testing.assert_array_equal(rows, shifted_window_rows(1, (96, 96, 96), (6, 6, 6), (3, 3, 3)))
+
+
+WATTN = [
+    # kind, C, heads, B, spatial, window, shift, cross
+    (0, 12, 6, 2, (1, 12, 12), (1, 6, 6), (0, 3, 3), False),
+    (0, 12, 6, 2, (1, 12, 12), (1, 6, 6), (0, 0, 0), True),
+    (0, 12, 6, 2, (1, 12, 18), (1, 6, 6), (0, 3, 3), True),
+    (0, 12, 6, 1, (12, 12, 12), (6, 6, 6), (3, 3, 3), False),
+    (0, 12, 6, 1, (12, 12, 12), (6, 6, 6), (3, 3, 3), True),
+    (0, 12, 6, 2, (1, 6, 6), (1, 3, 3), (0, 1, 1), False),
+    (0, 24, 12, 1, (1, 12, 12), (1, 6, 6), (0, 3, 3), False),
+    (0, 6, 3, 2, (1, 12, 12), (1, 6, 6), (0, 3, 3), False),
+    (1, 12, 3, 2, (1, 12, 12), (1, 6, 6), (0, 3, 3), False),
+    (1, 12, 3, 1, (12, 12, 12), (6, 6, 6), (3, 3, 3), False),
+    (1, 24, 6, 2, (1, 6, 6), (1, 6, 6), (0, 0, 0), False),
+    (1, 24, 6, 1, (6, 6, 6), (6, 6, 6), (0, 0, 0), False),
+    (1, 48, 12, 2, (1, 3, 3), (1, 3, 3), (0, 0, 0), False),
+    (1, 48, 12, 2, (3, 3, 3), (3, 3, 3), (0, 0, 0), False),
+    (0, 12, 6, 1, (12, 24, 6), (6, 6, 6), (3, 3, 3), False),
+]
+
+
+@pytest.mark.parametrize("kind,C,heads,B,spatial,window,shift,cross", WATTN)
+def test_window_attention_fwd_bwd_vs_oracle(device, kind, C, heads, B, spatial, window, shift, cross):
+    gen = torch.Generator().manual_seed(hash((kind, C, B, spatial, window, shift, cross)) % (2 ** 31))
+    geom = MF.WindowGeometry(B, spatial, window, shift)
+    rows = geom.tokens
+    Tsz = geom.table_rows
+    q = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    k = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    v = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    table = torch.randn(Tsz, heads, generator=gen, dtype=torch.float64) * (0.5 if kind == 0 else 4.0)
+    tau = (torch.rand(heads, generator=gen, dtype=torch.float64) * 15 + 5) if kind == 1 else None
+    gout = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    scale = (C // heads) ** -0.5
+    # oracle (float64, CPU, autograd)
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v, table)]
+    tau_l = tau.clone().requires_grad_(True) if tau is not None else None
+    ref = O.window_attention(*leaves, B, spatial, window, shift, heads, kind, scale=scale, tau=tau_l)
+    (ref * gout).sum().backward()
+    # HIP kernel (fp32)
+    f = lambda t: t.float().to(device).requires_grad_(True)  # noqa: E731
+    tab_d = f(table)
+    tau_d = f(tau) if tau is not None else None
+    if cross:
+        qd = f(q)
+        kvd = f(torch.cat([k, v], dim=1))
+        out = MF.window_attention_cross(qd, kvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
+    else:
+        qkvd = f(torch.cat([q, k, v], dim=1))
+        out = MF.window_attention_self(qkvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
+    (out * gout.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    if cross:
+        dq, dk, dv = qd.grad, kvd.grad[:, :C], kvd.grad[:, C:]
+    else:
+        dq, dk, dv = qkvd.grad[:, :C], qkvd.grad[:, C:2 * C], qkvd.grad[:, 2 * C:]
+    assert rel_err(dq, leaves[0].grad) < TOL
+    assert rel_err(dk, leaves[1].grad) < TOL
+    assert rel_err(dv, leaves[2].grad) < TOL
+    assert rel_err(tab_d.grad, leaves[3].grad) < TOL
+    if tau is not None:
+        assert rel_err(tau_d.grad, tau_l.grad) < TOL
+
+
+def test_window_attention_large_logits_and_masking(device):
+    """Saturated logits (large tau and bias) stay finite and match the oracle: exercises the
+    online-max rescale and the -100 mask interplay."""
+    B, spatial, window, shift, C, heads = 1, (1, 12, 12), (1, 6, 6), (0, 3, 3), 12, 3
+    geom = MF.WindowGeometry(B, spatial, window, shift)
+    gen = torch.Generator().manual_seed(7)
+    q = torch.randn(geom.tokens, C, generator=gen, dtype=torch.float64)
+    k = q + 0.01 * torch.randn(geom.tokens, C, generator=gen, dtype=torch.float64)
+    v = torch.randn(geom.tokens, C, generator=gen, dtype=torch.float64)
+    table = torch.randn(geom.table_rows, heads, generator=gen, dtype=torch.float64) * 16
+    tau = torch.full((heads,), 100.0, dtype=torch.float64)
+    ref = O.window_attention(q, k, v, table, B, spatial, window, shift, heads, 1, tau=tau)
+    qkv = torch.cat([q, k, v], 1).float().to(device)
+    out = MF.window_attention_self(qkv, table.float().to(device), geom, heads, kind=1, tau=tau.float().to(device))
+    assert torch.isfinite(out).all()
+    assert rel_err(out, ref) < TOL
+
+
+MHA = [
+    # Tq, Tk, B, heads, hd, causal
+    (16, 16, 2, 12, 7, True),
+    (368, 368, 2, 12, 7, True),
+    (50, 70, 2, 12, 14, True),
+    (70, 50, 2, 12, 14, True),
+    (64, 64, 3, 4, 16, False),
+    (33, 47, 1, 2, 8, False),
+    (200, 200, 2, 12, 14, True),
+    (130, 130, 1, 6, 4, True),
+]
+
+
+@pytest.mark.parametrize("Tq,Tk,B,heads,hd,causal", MHA)
+def test_mha_fwd_bwd_vs_oracle(device, Tq, Tk, B, heads, hd, causal):
+    gen = torch.Generator().manual_seed(Tq * 1000 + Tk + hd)
+    E = heads * hd
+    q, k, v = [torch.randn(T, B, E, generator=gen, dtype=torch.float64) for T in (Tq, Tk, Tk)]
+    gout = torch.randn(Tq, B, E, generator=gen, dtype=torch.float64)
+    diag = O.causal_diag(Tq, Tk) if causal else 0
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    ref, ref_w = O.mha_core(*leaves, heads, diag)
+    (ref * gout).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (q, k, v)]
+    out, lse = MF.mha_core(*dev, heads, diag)
+    (out * gout.float().to(device)).sum().backward()
+    w = MF.mha_mean_probs(dev[0], dev[1], lse, heads, diag)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    assert rel_err(w, ref_w) < TOL
+    for a, b in zip(dev, leaves):
+        assert rel_err(a.grad, b.grad) < TOL
+
+
+CONV = [
+    # B, (D,H,W), Cin, Cout, k, stride, pad, slope
+    (2, (16, 16, 16), 1, 12, (8, 8, 8), (8, 8, 8), (0, 0, 0), 1.0),
+    (2, (10, 12, 14), 6, 12, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
+    (1, (8, 8, 8), 24, 12, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
+    (2, (9, 9, 9), 3, 1, (3, 3, 3), (1, 1, 1), (1, 1, 1), 1.0),
+    (1, (9, 9, 9), 1, 6, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
+    (1, (9, 9, 9), 12, 6, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
+    (1, (9, 9, 9), 6, 3, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
+    (2, (1, 20, 24), 6, 12, (1, 3, 3), (1, 1, 1), (0, 1, 1), 0.2),
+    (2, (1, 84, 84), 1, 12, (1, 7, 7), (1, 7, 7), (0, 0, 0), 1.0),
+]
+
+
+@pytest.mark.parametrize("B,sp,Cin,Cout,k,stride,pad,slope", CONV)
+def test_conv3d_fwd_bwd_vs_oracle(device, B, sp, Cin, Cout, k, stride, pad, slope):
+    gen = torch.Generator().manual_seed(Cin * 100 + Cout + sum(sp))
+    x = torch.randn(B, *sp, Cin, generator=gen, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, *k, generator=gen, dtype=torch.float64) * 0.2
+    b = torch.randn(Cout, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    ref = O.conv3d_cl(*leaves, stride, pad, slope)
+    gout = torch.randn(ref.shape, generator=gen, dtype=torch.float64)
+    (ref * gout).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b)]
+    out = MF.conv3d_cl(*dev, stride, pad, slope)
+    (out * gout.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    for a, r in zip(dev, leaves):
+        assert rel_err(a.grad, r.grad) < TOL
