@@ -15,6 +15,46 @@ from ._lib import check, ptr, require_device, stream_handle
 LN100 = math.log(1.0 / 0.01)
 
 
+class KernelTimer:
+    """Optional per-launch timing of the hot kernels with HIP events recorded on the stream the
+    kernel is launched on (torch's current stream).  Off by default; bench.py enables it over its
+    timed region.  records[name] = list of (start_event, end_event, algorithmic_flops, bytes)."""
+    enabled = False
+    records = {}
+
+    @classmethod
+    def start(cls):
+        if not cls.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    @classmethod
+    def stop(cls, name, ev, flops, nbytes):
+        if ev is None:
+            return
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        cls.records.setdefault(name, []).append((ev, end, flops, nbytes))
+
+    @classmethod
+    def summary(cls):
+        """{name: dict(launches, total_ms, avg_ms, flops_per_launch, bytes_per_launch)} (syncs)."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, recs in cls.records.items():
+            ms = [a.elapsed_time(b) for a, b, _, _ in recs]
+            out[name] = dict(launches=len(recs), total_ms=sum(ms), avg_ms=sum(ms) / len(ms),
+                             flops_per_launch=sum(r[2] for r in recs) / len(recs),
+                             bytes_per_launch=sum(r[3] for r in recs) / len(recs))
+        return out
+
+    @classmethod
+    def reset(cls):
+        cls.records = {}
+
+
 @dataclass(frozen=True)
 class WindowGeometry:
     """Volume grid + window + cyclic shift of one shifted-window attention call.
@@ -102,8 +142,11 @@ class _WindowAttention(torch.autograd.Function):
         v = kv_src[:, v_off:]
         d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
+        ev = KernelTimer.start()
         check(L.mmni_wattn_fwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau_c), ptr(out), ptr(lse),
                                stream_handle(q_src.device)), "mmni_wattn_fwd")
+        # SURVEY §8d counting: fwd 4*T*N*C FLOPs, 4*T*C*4 bytes (q, k, v read, o written)
+        KernelTimer.stop(f"wattn_fwd_k{kind}_C{C}_N{geom.N}", ev, 4.0 * rows * geom.N * C, 16.0 * rows * C)
         ctx.save_for_backward(q_src, kv_src, table, tau_c, out, lse)
         ctx.cfg = (geom, heads, kind, scale, k_off, v_off, packed, C)
         return out
@@ -127,9 +170,14 @@ class _WindowAttention(torch.autograd.Function):
         dq, dk, dv = dq_src, dkv_src[:, k_off:], dkv_src[:, v_off:]
         d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
+        ev = KernelTimer.start()
         check(L.mmni_wattn_bwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau), ptr(out), ptr(dout), ptr(lse),
                                ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau),
                                stream_handle(q_src.device)), "mmni_wattn_bwd")
+        # SURVEY §8d counting: bwd 10*T*N*C FLOPs; bytes 8*T*C*4 + 4*T*heads (lse)
+        rows = q_src.shape[0]
+        KernelTimer.stop(f"wattn_bwd_k{kind}_C{C}_N{geom.N}", ev, 10.0 * rows * geom.N * C,
+                         32.0 * rows * C + 4.0 * rows * heads)
         if packed:
             return dq_src, None, dtable, dtau, None, None, None, None, None, None, None
         return dq_src, dkv_src, dtable, dtau, None, None, None, None, None, None, None
@@ -207,8 +255,10 @@ class _MHA(torch.autograd.Function):
         out = torch.empty((Tq, B, E), device=q.device, dtype=torch.float32)
         lse = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
         d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        ev = KernelTimer.start()
         check(_lib.load().mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse),
                                         stream_handle(q.device)), "mmni_mha_fwd")
+        KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.cfg = (heads, causal_diag, scale)
         ctx.mark_non_differentiable(lse)
@@ -226,9 +276,11 @@ class _MHA(torch.autograd.Function):
         dv = torch.empty_like(v)
         ws = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
         d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        ev = KernelTimer.start()
         check(_lib.load().mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
                                         ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
               "mmni_mha_bwd")
+        KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
         return dq, dk, dv, None, None, None
 
 
@@ -293,8 +345,12 @@ class _Conv3d(torch.autograd.Function):
         assert weight.dim() == 5 and x.dim() == 5 and x.shape[-1] == weight.shape[1]
         d = _conv_desc(tuple(x.shape), tuple(weight.shape), stride, pad, slope)
         y = torch.empty((d.B, d.Do, d.Ho, d.Wo, d.Cout), device=x.device, dtype=torch.float32)
+        ev = KernelTimer.start()
         check(_lib.load().mmni_conv3d_fwd(d, ptr(x), ptr(weight), ptr(bias), ptr(y), stream_handle(x.device)),
               "mmni_conv3d_fwd")
+        nout = y.numel() // d.Cout
+        KernelTimer.stop(f"conv3d_fwd_{d.Cin}x{d.Cout}_k{d.kd}{d.kh}{d.kw}", ev,
+                         2.0 * nout * d.Cout * d.Cin * d.kd * d.kh * d.kw, 4.0 * (x.numel() + y.numel()))
         ctx.save_for_backward(x, weight, y if slope != 1.0 else None)
         ctx.cfg = (stride, pad, slope, bias is not None)
         return y
@@ -308,8 +364,13 @@ class _Conv3d(torch.autograd.Function):
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         dw = torch.zeros_like(weight)
         db = torch.zeros(d.Cout, device=x.device, dtype=torch.float32) if has_bias else None
+        ev = KernelTimer.start()
         check(_lib.load().mmni_conv3d_bwd(d, ptr(x), ptr(weight), ptr(y), ptr(dy), ptr(dx), ptr(dw), ptr(db),
                                            stream_handle(x.device)), "mmni_conv3d_bwd")
+        nout = dy.numel() // d.Cout
+        KernelTimer.stop(f"conv3d_bwd_{d.Cin}x{d.Cout}_k{d.kd}{d.kh}{d.kw}", ev,
+                         4.0 * nout * d.Cout * d.Cin * d.kd * d.kh * d.kw,
+                         4.0 * (2 * x.numel() + 2 * dy.numel()))
         return dx, dw, db, None, None, None
 
 

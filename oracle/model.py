@@ -167,6 +167,11 @@ def _conv(p, name, x_cl, slope):
 def swinfusion_logits(p, A, Bv, cfg):
     """cfg: dict(window_size, patch_size, Ex_depths, Fusion_depths, Re_depths, heads (int),
     resolution (patches resolution tuple), head_patch)."""
+    return swin_v2_logits(p, "swin.", swinfusion_trunk(p, A, Bv, cfg), cfg["head_patch"], cfg["window_size"])
+
+
+def swinfusion_trunk(p, A, Bv, cfg):
+    """Ex / Fusion / Re trunk of SwinFusion (model.py:1396-1482): pair -> fused map (B, *spatial)."""
     ws = cfg["window_size"]
     res = tuple(cfg["resolution"])
     heads = cfg.get("heads", 6)
@@ -206,8 +211,7 @@ def swinfusion_logits(p, A, Bv, cfg):
     z = unembed(_ln(p, "norm_Re", t), x_size)
     z = _conv(p, "conv_last1", z, 0.2)
     z = _conv(p, "conv_last2", z, 0.2)
-    z = _conv(p, "conv_last3", z, 1.0)[..., 0]
-    return swin_v2_logits(p, "swin.", z, cfg["head_patch"], ws)
+    return _conv(p, "conv_last3", z, 1.0)[..., 0]
 
 
 def params_of(module, dtype=torch.float64):
