@@ -66,15 +66,17 @@ def synthetic_pairs(n, size, device, seed):
     return A, B, y
 
 
-def latest_pmc(kernel_prefix):
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+def latest_pmc(kernel_name):
+    """HBM bytes per launch of `kernel_name` (bench naming, e.g. wattn_bwd_k0_C12_N216) from the
+    newest committed PMC summary (scripts/summarize_profile.py), or (None, None)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.startswith(kernel_prefix) and v.get("hbm_bytes_per_launch") is not None:
+            if kernel_name.startswith(k + "_") and v.get("hbm_bytes_per_launch") is not None:
                 return v["hbm_bytes_per_launch"], os.path.basename(f)
     return None, None
 
@@ -171,7 +173,7 @@ def main():
         roofline = None
         if dom is not None:
             tflops = dom["flops_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e12
-            traffic, pmc_file = latest_pmc(dom_name.split("_k")[0])
+            traffic, pmc_file = latest_pmc(dom_name)
             roofline = dict(kernel=dom_name, bound="mfma", achieved=round(tflops, 3), peak=FP32_PEAK_TFLOPS,
                             unit="TFLOP/s", frac=round(tflops / FP32_PEAK_TFLOPS, 4), traffic=traffic,
                             avg_ms=round(dom["avg_ms"], 4), launches_per_step=dom["launches"] / args.steps,
