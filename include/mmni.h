@@ -22,6 +22,7 @@
 #ifndef MMNI_H
 #define MMNI_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -80,13 +81,17 @@ int mmni_wattn_fwd(const mmni_wattn_desc* d,
 
 /* Backward (flash-style recompute from lse).  dq/dk/dv are fully overwritten (every token
  * belongs to exactly one window).  dtable (Tsz, heads) and dtau (heads) are ACCUMULATED
- * with atomics: the caller zeroes them.  dtau may be NULL for kind 0. */
+ * (dtable += grad): the caller zeroes them.  dtau may be NULL for kind 0.
+ * workspace: >= mmni_wattn_bwd_workspace_bytes(d) bytes, 8-byte aligned, contents ignored
+ * (the library zeroes it on the stream); it holds the 64-bit fixed-point table gradient, which
+ * makes dtable bitwise deterministic. */
+size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d);
 int mmni_wattn_bwd(const mmni_wattn_desc* d,
                    const float* q, const float* k, const float* v,
                    const float* table, const float* tau,
                    const float* out, const float* dout, const float* lse,
                    float* dq, float* dk, float* dv,
-                   float* dtable, float* dtau, void* stream);
+                   float* dtable, float* dtau, void* workspace, void* stream);
 
 /* Integer maps the attention kernels use, exported for bit-exact parity tests (row a0).
  *   mmni_window_rows:   rows[w*N + t] = source token row of window-local token t of window w

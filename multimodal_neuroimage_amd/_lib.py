@@ -48,7 +48,8 @@ SIGNATURES = {
     "mmni_version": (_c_int, []),
     "mmni_last_error": (ctypes.c_char_p, []),
     "mmni_wattn_fwd": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 14),
+    "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 15),
+    "mmni_wattn_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WAttnDesc)]),
     "mmni_window_rows": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
     "mmni_window_mask": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
     "mmni_relative_index": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),

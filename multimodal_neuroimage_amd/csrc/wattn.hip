@@ -96,11 +96,28 @@ struct WAArgs {
     float* dv;
     float* dtable;
     float* dtau;
+    unsigned long long* dtab_fix;   // global int64 fixed-point accumulator (workspace)
 };
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
 constexpr float kNormEps = 1e-12f;          // F.normalize eps (swin_v2_module.py:153)
 constexpr int CH = 4;                       // keys per online-softmax chunk
+
+// The bias-table gradient is a scatter-add of N*N*heads values per window into a
+// (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
+// backward on gfx950 (measured: 27.8 ms vs 4.8 ms without the table update at the C3 shape),
+// integer LDS atomics run at full rate.  So the table gradient is accumulated in 64-bit fixed
+// point (2^-32 resolution, +-2^31 range): exact, order-independent integer adds, i.e. bitwise
+// deterministic, flushed to a global int64 workspace and converted once.
+constexpr double kFixScale = 4294967296.0;   // 2^32
+__device__ __forceinline__ unsigned long long to_fixed(float x) {
+    // x * 2^32 without a slow f32 -> i64 conversion: integer part and 31-bit fraction separately
+    const float xi = truncf(x);
+    const int hi = (int)xi;                                   // |x| < 2^31 assumed
+    const int lo = (int)((x - xi) * 2147483648.0f);           // |x - xi| < 1, exact scale 2^31
+    const long long v = (long long)hi * 4294967296LL + (long long)lo * 2LL;
+    return (unsigned long long)v;
+}
 
 template <int C>
 __device__ __forceinline__ void load_row(float (&dst)[C], const float* src) {
@@ -320,18 +337,22 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_kernel(WAArgs a) {
 // ------------------------------------------------------------------------------------
 template <int C, int HD, int KIND, int MAXT>
 __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
+    // LDS: one region R reused by both passes (K/V rows for pass A, then a2/dO + lse/delta rows
+    // for pass B), plus key metadata, the bias table and the fixed-point table gradient.
     constexpr int NH = C / HD;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WGeom& g = a.g;
     const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB;
     const int T = WPB * NPAD;
-    float* qd_s = smem;                                  // [T][2C]  a2 = prescaled q, dO
-    float* kv_s = qd_s + (size_t)T * 2 * C;              // [T][2C]  k (k-hat for kind 1), v
-    float* rs_s = kv_s + (size_t)T * 2 * C;              // [T][2*NH] lse2, delta
-    int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)T * 2 * NH);  // [T]
+    float* R = smem;                                      // max(T*2C, T*(2C + 2NH)) floats
+    float* kv_s = R;                                      // pass A: [T][2C] k (k-hat), v
+    float* qd_s = R;                                      // pass B: [T][2C] a2, dO
+    float* rs_s = R + (size_t)T * 2 * C;                  // pass B: [T][2NH] lse2, delta
+    int2* meta_s = reinterpret_cast<int2*>(R + (size_t)T * (2 * C + 2 * NH));   // [T]
     float* tab_s = reinterpret_cast<float*>(meta_s + T); // [Tsz][NH] (log2 domain)
-    float* dtab_s = tab_s + g.Tsz * NH;                  // [Tsz][NH] natural-domain grad
-    float* dtau_s = dtab_s + g.Tsz * NH;                 // [NH]
+    unsigned long long* dtab_s =                          // [Tsz][NH] grad, 64-bit fixed point
+        reinterpret_cast<unsigned long long*>(tab_s + ((g.Tsz * NH + 1) & ~1));
+    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * NH);   // [NH]
 
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -341,111 +362,103 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
 
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
         tab_s[e] = a.table[e] * kLog2e;
-        dtab_s[e] = 0.f;
+        dtab_s[e] = 0ull;
     }
     if (tid < NH) dtau_s[tid] = 0.f;
-
     float dtr[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) dtr[h] = 0.f;
 
     for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
-        // ---- stage the window group
+        const int w = grp * WPB + wl;
+        const bool active = (wl < WPB) && (w < g.nwin);
+        const int own = wl_c * NPAD + (active ? t : 0);
+        // ---- own row into registers: a2 (prescaled q), dO, lse2, delta
+        float aq[C], dO[C], lse2[NH], dl[NH];
+        int64_t row = 0;
+        int code = 0, rc = 0;
+        if (active) {
+            const TokenInfo ti = token_info(g, w, t);
+            row = ti.row;
+            code = ti.code;
+            rc = ti.rc;
+            load_row<C>(aq, a.q + row * a.qs);
+            if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(aq, nrm); }
+            float o[C];
+            load_row<C>(dO, a.dout + row * a.os);
+            load_row<C>(o, a.o + row * a.os);
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const float t2 = (KIND == 1) ? a.tau[h] * kLog2e : a.scale * kLog2e;
+                float dd = 0.f;
+#pragma unroll
+                for (int c = 0; c < HD; ++c) {
+                    aq[h * HD + c] *= t2;
+                    dd = fmaf(o[h * HD + c], dO[h * HD + c], dd);
+                }
+                lse2[h] = a.lse[row * NH + h] * kLog2e;
+                dl[h] = dd;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) { aq[c] = 0.f; dO[c] = 0.f; }
+#pragma unroll
+            for (int h = 0; h < NH; ++h) { lse2[h] = INFINITY; dl[h] = 0.f; }
+        }
+        // ---- stage K/V + metadata (owners write their row; pad rows get neutral values)
+        if (active && p == 0) {
+            float kr[C], vr[C];
+            load_row<C>(kr, a.k + row * a.ks);
+            if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
+            load_row<C>(vr, a.v + row * a.vs);
+            store_row<C>(kv_s + (size_t)own * 2 * C, kr);
+            store_row<C>(kv_s + (size_t)own * 2 * C + C, vr);
+            meta_s[own] = make_int2(code | (rc << 16), 0);
+        }
         for (int e = tid; e < T; e += blockDim.x) {
             const int w2 = e / NPAD, t2 = e - w2 * NPAD;
-            const int w = grp * WPB + w2;
-            float x0[C], x1[C];
-            float* rs = rs_s + (size_t)e * 2 * NH;
-            if (t2 < N && w < g.nwin) {
-                const TokenInfo ti = token_info(g, w, t2);
-                // q -> a2
-                load_row<C>(x0, a.q + ti.row * a.qs);
-                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(x0, nrm); }
+            if (t2 >= N || grp * WPB + w2 >= g.nwin) {
+                float z[C];
 #pragma unroll
-                for (int h = 0; h < NH; ++h) {
-                    const float t2 = (KIND == 1) ? a.tau[h] * kLog2e : a.scale * kLog2e;
-#pragma unroll
-                    for (int c = 0; c < HD; ++c) x0[h * HD + c] *= t2;
-                }
-                load_row<C>(x1, a.dout + ti.row * a.os);
-                store_row<C>(qd_s + (size_t)e * 2 * C, x0);
-                store_row<C>(qd_s + (size_t)e * 2 * C + C, x1);
-                // delta = rowsum(dO * O) per head
-                load_row<C>(x0, a.o + ti.row * a.os);
-#pragma unroll
-                for (int h = 0; h < NH; ++h) {
-                    float dd = 0.f;
-#pragma unroll
-                    for (int c = 0; c < HD; ++c) dd = fmaf(x0[h * HD + c], x1[h * HD + c], dd);
-                    rs[h] = a.lse[ti.row * NH + h] * kLog2e;
-                    rs[NH + h] = dd;
-                }
-                load_row<C>(x0, a.k + ti.row * a.ks);
-                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(x0, nrm); }
-                load_row<C>(x1, a.v + ti.row * a.vs);
-                store_row<C>(kv_s + (size_t)e * 2 * C, x0);
-                store_row<C>(kv_s + (size_t)e * 2 * C + C, x1);
-                meta_s[e] = make_int2(ti.code | (ti.rc << 16), 0);
-            } else {
-#pragma unroll
-                for (int c = 0; c < C; ++c) x0[c] = 0.f;
-                store_row<C>(qd_s + (size_t)e * 2 * C, x0);
-                store_row<C>(qd_s + (size_t)e * 2 * C + C, x0);
-                store_row<C>(kv_s + (size_t)e * 2 * C, x0);
-                store_row<C>(kv_s + (size_t)e * 2 * C + C, x0);
-#pragma unroll
-                for (int h = 0; h < NH; ++h) { rs[h] = INFINITY; rs[NH + h] = 0.f; }
+                for (int c = 0; c < C; ++c) z[c] = 0.f;
+                store_row<C>(kv_s + (size_t)e * 2 * C, z);
+                store_row<C>(kv_s + (size_t)e * 2 * C + C, z);
                 meta_s[e] = make_int2(0, __float_as_int(-INFINITY));
             }
         }
         __syncthreads();
-
-        const int w = grp * WPB + wl;
-        const bool active = (wl < WPB) && (w < g.nwin);
-        const int own = wl_c * NPAD + (active ? t : 0);
-        const int2 mown = meta_s[own];
-        const int cown = mown.x & 0xffff, rown = mown.x >> 16;
-        const float* qdw = qd_s + (size_t)wl_c * NPAD * 2 * C;
-        const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
-        const float* rsw = rs_s + (size_t)wl_c * NPAD * 2 * NH;
         const int2* mw = meta_s + wl_c * NPAD;
         const int nk = NPAD / KS;
 
         // ================= pass A: lane = query row -> dq, dtable, dtau
         {
-            float aq[C], dO[C], lse2[NH], dl[NH], dqa[C];
-            load_row<C>(aq, qd_s + (size_t)own * 2 * C);
-            load_row<C>(dO, qd_s + (size_t)own * 2 * C + C);
-#pragma unroll
-            for (int h = 0; h < NH; ++h) {
-                lse2[h] = active ? rs_s[(size_t)own * 2 * NH + h] : INFINITY;
-                dl[h] = rs_s[(size_t)own * 2 * NH + NH + h];
-            }
+            const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
+            float dqa[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) dqa[c] = 0.f;
-            const int cq = cown + g.off;
+            const int cq = code + g.off;
             for (int n = 0; n < nk; ++n) {
                 const int j = p + KS * n;
                 const int2 mt = mw[j];
-                const int code = mt.x & 0xffff, rcj = mt.x >> 16;
-                const float madd = (rcj == rown ? 0.f : kMask2) + __int_as_float(mt.y);
-                const int tix = (cq - code) * NH;
-                float kr[C], vr[C];
-                load_row<C>(kr, kvw + (size_t)j * 2 * C);
-                load_row<C>(vr, kvw + (size_t)j * 2 * C + C);
+                const int kcode = mt.x & 0xffff, rcj = mt.x >> 16;
+                const float madd = (rcj == rc ? 0.f : kMask2) + __int_as_float(mt.y);
+                const int tix = (cq - kcode) * NH;
+                float kj[C], vj[C];
+                load_row<C>(kj, kvw + (size_t)j * 2 * C);
+                load_row<C>(vj, kvw + (size_t)j * 2 * C + C);
 #pragma unroll
                 for (int h = 0; h < NH; ++h) {
                     float dot = 0.f, dp = 0.f;
 #pragma unroll
                     for (int c = 0; c < HD; ++c) {
-                        dot = fmaf(aq[h * HD + c], kr[h * HD + c], dot);
-                        dp = fmaf(dO[h * HD + c], vr[h * HD + c], dp);
+                        dot = fmaf(aq[h * HD + c], kj[h * HD + c], dot);
+                        dp = fmaf(dO[h * HD + c], vj[h * HD + c], dp);
                     }
                     const float pr = fast_exp2(dot + tab_s[tix + h] + madd - lse2[h]);
                     const float ds = pr * (dp - dl[h]);
 #pragma unroll
-                    for (int c = 0; c < HD; ++c) dqa[h * HD + c] = fmaf(ds, kr[h * HD + c], dqa[h * HD + c]);
-                    atomicAdd(&dtab_s[tix + h], ds);
+                    for (int c = 0; c < HD; ++c) dqa[h * HD + c] = fmaf(ds, kj[h * HD + c], dqa[h * HD + c]);
+                    atomicAdd(&dtab_s[tix + h], to_fixed(ds));
                     if constexpr (KIND == 1) dtr[h] = fmaf(ds, dot, dtr[h]);
                 }
             }
@@ -454,11 +467,10 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
                 for (int c = 0; c < C; ++c) dqa[c] += __shfl_xor(dqa[c], o);
             }
             if (active && p == 0) {
-                const TokenInfo ti = token_info(g, w, t);
                 float dq[C];
                 if (KIND == 1) {
                     float qr[C], nrm[NH];
-                    load_row<C>(qr, a.q + ti.row * a.qs);
+                    load_row<C>(qr, a.q + row * a.qs);
                     normalize_heads<C, HD>(qr, nrm);
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
@@ -471,42 +483,72 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
 #pragma unroll
                     for (int c = 0; c < C; ++c) dq[c] = dqa[c] * a.scale;
                 }
-                store_row<C>(a.dq + ti.row * a.qs, dq);
+                store_row<C>(a.dq + row * a.qs, dq);
             }
         }
+        __syncthreads();
+        // ---- restage: a2/dO and lse2/delta rows for pass B (owners from registers)
+        if (active && p == 0) {
+            store_row<C>(qd_s + (size_t)own * 2 * C, aq);
+            store_row<C>(qd_s + (size_t)own * 2 * C + C, dO);
+            float* rs = rs_s + (size_t)own * 2 * NH;
+#pragma unroll
+            for (int h = 0; h < NH; ++h) { rs[h] = lse2[h]; rs[NH + h] = dl[h]; }
+        }
+        for (int e = tid; e < T; e += blockDim.x) {
+            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+            if (t2 >= N || grp * WPB + w2 >= g.nwin) {
+                float z[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) z[c] = 0.f;
+                store_row<C>(qd_s + (size_t)e * 2 * C, z);
+                store_row<C>(qd_s + (size_t)e * 2 * C + C, z);
+                float* rs = rs_s + (size_t)e * 2 * NH;
+#pragma unroll
+                for (int h = 0; h < NH; ++h) { rs[h] = INFINITY; rs[NH + h] = 0.f; }
+            }
+        }
+        __syncthreads();
 
         // ================= pass B: lane = key row -> dk, dv
         {
+            const float* qdw = qd_s + (size_t)wl_c * NPAD * 2 * C;
+            const float* rsw = rs_s + (size_t)wl_c * NPAD * 2 * NH;
             float kr[C], vr[C], dka[C], dva[C];
-            load_row<C>(kr, kv_s + (size_t)own * 2 * C);
-            load_row<C>(vr, kv_s + (size_t)own * 2 * C + C);
+            if (active) {
+                load_row<C>(kr, a.k + row * a.ks);
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
+                load_row<C>(vr, a.v + row * a.vs);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) { kr[c] = 0.f; vr[c] = 0.f; }
+            }
 #pragma unroll
             for (int c = 0; c < C; ++c) { dka[c] = 0.f; dva[c] = 0.f; }
-            const int ck = cown - g.off;
             for (int n = 0; n < nk; ++n) {
                 const int i = p + KS * n;
                 const int2 mt = mw[i];
-                const int code = mt.x & 0xffff, rci = mt.x >> 16;
-                const float madd = (rci == rown ? 0.f : kMask2) + __int_as_float(mt.y);
-                const int tix = (code - ck) * NH;
-                float aq[C], dO[C];
-                load_row<C>(aq, qdw + (size_t)i * 2 * C);
-                load_row<C>(dO, qdw + (size_t)i * 2 * C + C);
+                const int qcode = mt.x & 0xffff, rci = mt.x >> 16;
+                const float madd = (rci == rc ? 0.f : kMask2) + __int_as_float(mt.y);
+                const int tix = (qcode - code + g.off) * NH;
+                float ai[C], gi[C];
+                load_row<C>(ai, qdw + (size_t)i * 2 * C);
+                load_row<C>(gi, qdw + (size_t)i * 2 * C + C);
                 const float* rsi = rsw + (size_t)i * 2 * NH;
 #pragma unroll
                 for (int h = 0; h < NH; ++h) {
                     float dot = 0.f, dp = 0.f;
 #pragma unroll
                     for (int c = 0; c < HD; ++c) {
-                        dot = fmaf(aq[h * HD + c], kr[h * HD + c], dot);
-                        dp = fmaf(dO[h * HD + c], vr[h * HD + c], dp);
+                        dot = fmaf(ai[h * HD + c], kr[h * HD + c], dot);
+                        dp = fmaf(gi[h * HD + c], vr[h * HD + c], dp);
                     }
                     const float pr = fast_exp2(dot + tab_s[tix + h] + madd - rsi[h]);
                     const float ds = pr * (dp - rsi[NH + h]);
 #pragma unroll
                     for (int c = 0; c < HD; ++c) {
-                        dva[h * HD + c] = fmaf(pr, dO[h * HD + c], dva[h * HD + c]);
-                        dka[h * HD + c] = fmaf(ds, aq[h * HD + c], dka[h * HD + c]);
+                        dva[h * HD + c] = fmaf(pr, gi[h * HD + c], dva[h * HD + c]);
+                        dka[h * HD + c] = fmaf(ds, ai[h * HD + c], dka[h * HD + c]);
                     }
                 }
             }
@@ -518,11 +560,10 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
                 }
             }
             if (active && p == 0) {
-                const TokenInfo ti = token_info(g, w, t);
                 float dk[C];
                 if (KIND == 1) {
                     float kraw[C], nrm[NH];
-                    load_row<C>(kraw, a.k + ti.row * a.ks);
+                    load_row<C>(kraw, a.k + row * a.ks);
                     normalize_heads<C, HD>(kraw, nrm);
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
@@ -535,8 +576,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
 #pragma unroll
                     for (int c = 0; c < C; ++c) dk[c] = dka[c] * kLn2;
                 }
-                store_row<C>(a.dk + ti.row * a.ks, dk);
-                store_row<C>(a.dv + ti.row * a.vs, dva);
+                store_row<C>(a.dk + row * a.ks, dk);
+                store_row<C>(a.dv + row * a.vs, dva);
             }
         }
         __syncthreads();
@@ -553,13 +594,18 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     }
     __syncthreads();
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
-        const float v = dtab_s[e];
-        if (v != 0.f) atomicAdd(&a.dtable[e], v);
+        const unsigned long long v = dtab_s[e];
+        if (v != 0ull) atomicAdd(&a.dtab_fix[e], v);
     }
     if (KIND == 1 && tid < NH) {
         // dtau = sum ds * (q-hat . k-hat);  dot was taken against tau*log2e*q-hat
         atomicAdd(&a.dtau[tid], dtau_s[tid] / (a.tau[tid] * kLog2e));
     }
+}
+
+__global__ void wattn_dtable_convert_kernel(const unsigned long long* fix, float* dtable, int n) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) dtable[e] += (float)((double)(long long)fix[e] / kFixScale);
 }
 
 // ------------------------------------------------------------------------------------
@@ -640,7 +686,8 @@ struct WAConfig {
 static size_t wattn_lds_bytes(bool bwd, int C, int NH, int WPB, int NPAD, int Tsz) {
     const size_t T = (size_t)WPB * NPAD;
     if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
-    return T * 4 * C * 4 + T * 2 * NH * 4 + T * 8 + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
+    const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
+    return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
 }
 
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, WAConfig& cfg) {
@@ -755,15 +802,23 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     return 0;
 }
 
+extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
+    WGeom g;
+    if (make_geom(d, g)) return 0;
+    return (size_t)g.Tsz * d->heads * sizeof(unsigned long long);
+}
+
 extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
                               const float* table, const float* tau, const float* out, const float* dout,
                               const float* lse, float* dq, float* dk, float* dv, float* dtable, float* dtau,
-                              void* stream) {
+                              void* workspace, void* stream) {
     WAArgs a{};
     int HD = 0;
     int rc = fill_args(d, a, HD);
     if (rc) return rc;
-    MMNI_ARG_CHECK(q && k && v && table && out && dout && lse && dq && dk && dv && dtable, "wattn_bwd: null pointer");
+    MMNI_ARG_CHECK(q && k && v && table && out && dout && lse && dq && dk && dv && dtable && workspace,
+                   "wattn_bwd: null pointer");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(workspace) % 8 == 0, "wattn_bwd: workspace must be 8-byte aligned");
     MMNI_ARG_CHECK(d->kind == 0 || (tau != nullptr && dtau != nullptr), "wattn_bwd: kind 1 needs tau and dtau");
     MMNI_ARG_CHECK(row_aligned(q, d->q_stride, d->C) && row_aligned(k, d->k_stride, d->C) &&
                        row_aligned(v, d->v_stride, d->C) && row_aligned(out, d->o_stride, d->C) &&
@@ -780,12 +835,17 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;
+    a.dtab_fix = reinterpret_cast<unsigned long long*>(workspace);
     rc = ensure_lds_attr(kb, cfg.lds);
     if (rc) return rc;
+    const int ntab = a.g.Tsz * d->heads;
+    hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8, (hipStream_t)stream);
+    if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
     void* args[] = {&a};
-    hipError_t e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
+    e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
-    return 0;
+    wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, dtable, ntab);
+    return launch_status("wattn_dtable_convert");
 }
 
 extern "C" int mmni_window_rows(const mmni_wattn_desc* d, int32_t* rows, void* stream) {

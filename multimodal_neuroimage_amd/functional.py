@@ -170,9 +170,10 @@ class _WindowAttention(torch.autograd.Function):
         dq, dk, dv = dq_src, dkv_src[:, k_off:], dkv_src[:, v_off:]
         d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
+        ws = torch.empty(L.mmni_wattn_bwd_workspace_bytes(d) // 8, device=q_src.device, dtype=torch.int64)
         ev = KernelTimer.start()
         check(L.mmni_wattn_bwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau), ptr(out), ptr(dout), ptr(lse),
-                               ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau),
+                               ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau), ptr(ws),
                                stream_handle(q_src.device)), "mmni_wattn_bwd")
         # SURVEY §8d counting: bwd 10*T*N*C FLOPs; bytes 8*T*C*4 + 4*T*heads (lse)
         rows = q_src.shape[0]

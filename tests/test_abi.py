@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "mmni.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mmni_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mmni_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():
