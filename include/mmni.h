@@ -152,6 +152,24 @@ int mmni_conv3d_bwd(const mmni_conv3d_desc* d, const float* x, const float* w,
                     const float* y, const float* dy, float* dx, float* dw, float* db,
                     void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Token-wise ops of the Swin blocks: LayerNorm over C = 12/24/48/96
+ * channels (nn.LayerNorm semantics, swinfusion_module.py:300,306; swin_v2_module.py:233,240)
+ * and the weight gradient of a token Linear (dW = dY^T X, db = colsum dY) for the tall-skinny
+ * shapes of the qkv / proj / MLP layers.  Row-major (rows, C) / (rows, ld) tensors.
+ * Workspaces: caller-allocated, sizes from the *_workspace_bytes queries, contents ignored.
+ * dgamma / dbeta / dw / db are overwritten; reductions run in a fixed order (deterministic).
+ * ------------------------------------------------------------------------------------ */
+int mmni_layernorm_fwd(int64_t rows, int C, const float* x, const float* gamma, const float* beta,
+                       float eps, float* y, float* mean, float* rstd, void* stream);
+size_t mmni_layernorm_bwd_workspace_bytes(int64_t rows, int C);
+int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const float* x, const float* gamma,
+                       const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       void* workspace, void* stream);
+size_t mmni_linear_dw_workspace_bytes(int N, int K);
+int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy,
+                   int64_t lddy, float* dw, float* db, void* workspace, void* stream);
+
 int mmni_version(void);
 const char* mmni_last_error(void);
 

@@ -58,6 +58,11 @@ SIGNATURES = {
     "mmni_mha_mean_probs": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp]),
     "mmni_conv3d_fwd": (_c_int, [ctypes.POINTER(Conv3dDesc), _vp, _vp, _vp, _vp, _vp]),
     "mmni_conv3d_bwd": (_c_int, [ctypes.POINTER(Conv3dDesc)] + [_vp] * 8),
+    "mmni_layernorm_fwd": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp]),
+    "mmni_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
+    "mmni_layernorm_bwd": (_c_int, [_c_i64, _c_int] + [_vp] * 10),
+    "mmni_linear_dw_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int]),
+    "mmni_linear_dw": (_c_int, [_c_i64, _c_int, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

@@ -97,6 +97,7 @@ struct WAArgs {
     float* dtable;
     float* dtau;
     unsigned long long* dtab_fix;   // global int64 fixed-point accumulator (workspace)
+    unsigned int* maxbits;          // workspace tail: max|dout|, max|v| bits (fixed-point scale)
 };
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
@@ -107,16 +108,53 @@ constexpr int CH = 4;                       // keys per online-softmax chunk
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
 // backward on gfx950 (measured: 27.8 ms vs 4.8 ms without the table update at the C3 shape),
 // integer LDS atomics run at full rate.  So the table gradient is accumulated in 64-bit fixed
-// point (2^-32 resolution, +-2^31 range): exact, order-independent integer adds, i.e. bitwise
-// deterministic, flushed to a global int64 workspace and converted once.
-constexpr double kFixScale = 4294967296.0;   // 2^32
-__device__ __forceinline__ unsigned long long to_fixed(float x) {
-    // x * 2^32 without a slow f32 -> i64 conversion: integer part and 31-bit fraction separately
-    const float xi = truncf(x);
-    const int hi = (int)xi;                                   // |x| < 2^31 assumed
-    const int lo = (int)((x - xi) * 2147483648.0f);           // |x - xi| < 1, exact scale 2^31
+// point: exact, order-independent integer adds, i.e. bitwise deterministic, flushed to a global
+// int64 workspace and converted once.  The scale 2^S is picked per call from a proven bound so
+// the sum cannot overflow and keeps the most precision:
+//   |ds| = p |dO.v - delta| <= 2 * HD * max|dout| * max|v|          (delta is a p-average of dO.v)
+//   each query adds at most one ds per (entry, head)  =>  |entry sum| <= T * that bound
+//   S = 62 - ceil(log2(T * bound))
+// A fixed 2^-32 scale with truncation was measured at 20% error on BCE-loss-sized gradients
+// (table grads ~1e-7 made of ~1e4 contributions of ~1e-10); values are rounded to nearest.
+__device__ __forceinline__ int fix_exponent(const unsigned int* maxbits, int hd, long long T) {
+    const double bound = 2.0 * hd * (double)__uint_as_float(maxbits[0]) * (double)__uint_as_float(maxbits[1]) * (double)T;
+    if (!(bound < 1e300)) return 0;       // non-finite inputs: any scale, the result is garbage anyway
+    if (bound <= 0.0) return 150;
+    int ex;
+    frexp(bound, &ex);                    // bound < 2^ex
+    return max(-60, min(150, 62 - ex));
+}
+
+__device__ __forceinline__ unsigned long long to_fixed(float x, float ymul) {
+    // x * 2^S without a slow f32 -> i64 conversion: y = x * 2^(S-32) (exact), then the integer
+    // part of y and its fraction at 2^31 separately
+    const float y = x * ymul;
+    const float yi = truncf(y);
+    const int hi = (int)yi;                                   // |y| < 2^31 by the bound
+    const int lo = __float2int_rn((y - yi) * 2147483648.0f);  // y - yi exact, |.| < 1
     const long long v = (long long)hi * 4294967296LL + (long long)lo * 2LL;
     return (unsigned long long)v;
+}
+
+// max|dout| and max|v| for the fixed-point bound (non-negative float bits order as uints)
+__global__ void wattn_absmax_kernel(const float* dout, long long os, const float* v, long long vs, long long T,
+                                    int C, unsigned int* maxbits) {
+    float md = 0.f, mv = 0.f;
+    const long long n = T * C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / C;
+        const int c = (int)(i - r * C);
+        md = fmaxf(md, fabsf(dout[r * os + c]));
+        mv = fmaxf(mv, fabsf(v[r * vs + c]));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        md = fmaxf(md, __shfl_xor(md, o));
+        mv = fmaxf(mv, __shfl_xor(mv, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&maxbits[0], __float_as_uint(md));
+        atomicMax(&maxbits[1], __float_as_uint(mv));
+    }
 }
 
 template <int C>
@@ -365,6 +403,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
         dtab_s[e] = 0ull;
     }
     if (tid < NH) dtau_s[tid] = 0.f;
+    const float ymul = exp2f((float)(fix_exponent(a.maxbits, HD, (long long)g.nwin * N) - 32));
     float dtr[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) dtr[h] = 0.f;
@@ -458,7 +497,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
                     const float ds = pr * (dp - dl[h]);
 #pragma unroll
                     for (int c = 0; c < HD; ++c) dqa[h * HD + c] = fmaf(ds, kj[h * HD + c], dqa[h * HD + c]);
-                    atomicAdd(&dtab_s[tix + h], to_fixed(ds));
+                    atomicAdd(&dtab_s[tix + h], to_fixed(ds, ymul));
                     if constexpr (KIND == 1) dtr[h] = fmaf(ds, dot, dtr[h]);
                 }
             }
@@ -603,9 +642,10 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     }
 }
 
-__global__ void wattn_dtable_convert_kernel(const unsigned long long* fix, float* dtable, int n) {
+__global__ void wattn_dtable_convert_kernel(const unsigned long long* fix, const unsigned int* maxbits, int hd,
+                                            long long T, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dtable[e] += (float)((double)(long long)fix[e] / kFixScale);
+    if (e < n) dtable[e] += (float)ldexp((double)(long long)fix[e], -fix_exponent(maxbits, hd, T));
 }
 
 // ------------------------------------------------------------------------------------
@@ -805,7 +845,7 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
 extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
     WGeom g;
     if (make_geom(d, g)) return 0;
-    return (size_t)g.Tsz * d->heads * sizeof(unsigned long long);
+    return (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16;   // + the two absmax words
 }
 
 extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
@@ -839,12 +879,18 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     rc = ensure_lds_attr(kb, cfg.lds);
     if (rc) return rc;
     const int ntab = a.g.Tsz * d->heads;
-    hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8, (hipStream_t)stream);
+    a.maxbits = reinterpret_cast<unsigned int*>(a.dtab_fix + ntab);
+    hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8 + 16, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
+    const long long T = (long long)a.g.nwin * a.g.N;
+    wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C, a.maxbits);
+    rc = launch_status("wattn_absmax");
+    if (rc) return rc;
     void* args[] = {&a};
     e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
-    wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, dtable, ntab);
+    wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD, T,
+                                                                                     dtable, ntab);
     return launch_status("wattn_dtable_convert");
 }
 

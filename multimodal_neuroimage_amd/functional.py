@@ -8,6 +8,7 @@ from dataclasses import dataclass
 import math
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, ptr, require_device, stream_handle
@@ -379,3 +380,106 @@ def conv3d_cl(x, weight, bias=None, stride=1, pad=0, slope=1.0):
     """Channels-last conv: x (B, D, H, W, Cin), weight (Cout, Cin, kd, kh, kw) ->
     (B, Do, Ho, Wo, Cout) with a fused LeakyReLU(slope) (slope 1 = identity)."""
     return _Conv3d.apply(x, weight, bias, _triple(stride), _triple(pad), slope)
+
+
+# ----------------------------------------------------------------------------------------
+# token-wise LayerNorm and Linear (weight gradient on the f32 MFMA)
+# ----------------------------------------------------------------------------------------
+LN_CHANNELS = (12, 24, 48, 96)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        require_device(x, weight, bias, what="layer_norm")
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(_lib.load().mmni_layernorm_fwd(rows, C, ptr(x2), ptr(weight), ptr(bias), float(eps), ptr(y),
+                                              ptr(mean), ptr(rstd), stream_handle(x.device)), "mmni_layernorm_fwd")
+        KernelTimer.stop(f"layernorm_fwd_C{C}", ev, 8.0 * rows * C, 8.0 * rows * C + 8.0 * rows)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        C = x2.shape[1]
+        rows = x2.shape[0]
+        dy2 = dy.reshape(-1, C).contiguous()
+        dx = torch.empty_like(x2)
+        dgamma = torch.empty(C, device=x2.device, dtype=torch.float32)
+        dbeta = torch.empty(C, device=x2.device, dtype=torch.float32)
+        L = _lib.load()
+        ws = torch.empty(L.mmni_layernorm_bwd_workspace_bytes(rows, C) // 4, device=x2.device, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(L.mmni_layernorm_bwd(rows, C, ptr(dy2), ptr(x2), ptr(weight), ptr(mean), ptr(rstd), ptr(dx),
+                                   ptr(dgamma), ptr(dbeta), ptr(ws), stream_handle(x2.device)), "mmni_layernorm_bwd")
+        KernelTimer.stop(f"layernorm_bwd_C{C}", ev, 12.0 * rows * C, 12.0 * rows * C + 8.0 * rows)
+        return dx.view(ctx.shape), dgamma, dbeta, None
+
+
+def layer_norm(x, ln):
+    """nn.LayerNorm `ln` applied to x (..., C) with the HIP kernels (C in 12/24/48/96); other widths
+    (the crossmodal stack's 84/168) stay on torch's ROCm LayerNorm.  No CPU path."""
+    require_device(x, what="layer_norm")
+    C = x.shape[-1]
+    if C not in LN_CHANNELS:
+        return ln(x)
+    return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
+
+
+_DW_TILES = {(1, 1), (1, 2), (1, 3), (2, 1), (3, 1), (2, 2), (3, 3), (1, 4), (4, 1), (2, 3), (3, 2), (9, 3), (3, 9),
+             (6, 2), (2, 6), (4, 2), (2, 4), (5, 3), (3, 5), (6, 3), (3, 6), (8, 2), (2, 8), (12, 3), (3, 12),
+             (4, 4), (6, 6), (4, 12), (12, 4)}
+
+
+class _TokenLinear(torch.autograd.Function):
+    """y = x W^T + b on token rows; forward and dX on hipBLASLt (torch), dW/db on the HIP
+    MFMA reduction (the K = rows weight-gradient GEMM is where the library kernels stall)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        N, K = weight.shape
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = (dy2 @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
+        rows = x2.shape[0]
+        dw = torch.empty_like(weight)
+        db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
+        L = _lib.load()
+        ws = torch.empty(L.mmni_linear_dw_workspace_bytes(N, K) // 4, device=x.device, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(L.mmni_linear_dw(rows, N, K, ptr(x2), K, ptr(dy2), N, ptr(dw), ptr(db), ptr(ws),
+                               stream_handle(x.device)), "mmni_linear_dw")
+        KernelTimer.stop(f"linear_dw_{N}x{K}", ev, 2.0 * rows * N * K, 4.0 * rows * (N + K))
+        return dx, dw, db
+
+
+def linear(x, lin_or_weight, bias=None):
+    """Token Linear with the HIP weight-gradient kernel when the tile grid is supported."""
+    if isinstance(lin_or_weight, torch.nn.Linear):
+        weight, bias = lin_or_weight.weight, lin_or_weight.bias
+    else:
+        weight = lin_or_weight
+    require_device(x, what="linear")
+    N, K = weight.shape
+    if ((N + 15) // 16, (K + 15) // 16) not in _DW_TILES:
+        return F.linear(x, weight, bias)
+    return _TokenLinear.apply(x, weight, bias)

@@ -25,6 +25,7 @@ from .modules.swin_v2_module import BasicLayer, PatchEmbed, PatchMerging
 from .modules.swinfusion_module import (RSTB, CRSTB, PatchEmbed_fusion, PatchUnEmbed, Upsample, UpsampleOneStep,
                                         Cross_BasicLayer, conv_tokens)
 from .modules._common import trunc_normal_
+from .functional import layer_norm
 
 
 class BaseModel(nn.Module, ABC):
@@ -180,7 +181,7 @@ class SwinTransformerV2(BaseModel):
         x = self.pos_drop(x)
         for layer in self.layers:
             x = layer(x)
-        x = self.norm(x)
+        x = layer_norm(x, self.norm)
         return x.mean(dim=1)   # == AdaptiveAvgPool1d(1) over tokens, flattened
 
     def forward(self, x):
@@ -340,7 +341,7 @@ class SwinFusion(BaseModel):
         B, C = x_cl.shape[0], x_cl.shape[-1]
         t = x_cl.reshape(B, -1, C)
         if self.patch_embed.norm is not None:
-            t = self.patch_embed.norm(t)
+            t = layer_norm(t, self.patch_embed.norm)
         if self.ape:
             t = t + self.absolute_pos_embed
         return self.pos_drop(t)
@@ -356,7 +357,7 @@ class SwinFusion(BaseModel):
         t = self._embed(x)
         for layer in layers:
             t = layer(t, x_size)
-        return self._unembed(norm(t), x_size)
+        return self._unembed(layer_norm(t, norm), x_size)
 
     def forward_features_Ex_A(self, x_cl):
         return self._extract(x_cl, self.layers_Ex_A, self.norm_Ex_A)
@@ -370,8 +371,8 @@ class SwinFusion(BaseModel):
         x, y = self._embed(x_cl), self._embed(y_cl)
         for layer in self.layers_Fusion:
             x, y = layer(x, y, x_size)
-        x = self._unembed(self.norm_Fusion_A(x), x_size)
-        y = self._unembed(self.norm_Fusion_B(y), x_size)
+        x = self._unembed(layer_norm(x, self.norm_Fusion_A), x_size)
+        y = self._unembed(layer_norm(y, self.norm_Fusion_B), x_size)
         return conv_tokens(self.conv_after_body_Fusion, torch.cat([x, y], -1), 0.2)
 
     def forward_features_Re(self, x_cl):
@@ -379,7 +380,7 @@ class SwinFusion(BaseModel):
         t = self._embed(x_cl)
         for layer in self.layers_Re:
             t = layer(t, x_size)
-        x = self._unembed(self.norm_Re(t), x_size)
+        x = self._unembed(layer_norm(t, self.norm_Re), x_size)
         x = conv_tokens(self.conv_last1, x, 0.2)
         x = conv_tokens(self.conv_last2, x, 0.2)
         return conv_tokens(self.conv_last3, x, 1.0)

@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, conv3d_cl, LN100
+from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -33,7 +33,7 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+        return self.drop(linear(self.drop(self.act(linear(x, self.fc1))), self.fc2))
 
 
 def window_partition(x, window_size):
@@ -105,9 +105,9 @@ class WindowAttention(nn.Module):
         bias = None
         if self.q_bias is not None:
             bias = torch.cat((self.q_bias, torch.zeros_like(self.v_bias, requires_grad=False), self.v_bias))
-        qkv = F.linear(x, self.qkv.weight, bias)
+        qkv = linear(x, self.qkv.weight, bias)
         o = window_attention_self(qkv, self.bias_table(), geom, self.num_heads_swin, kind=1, tau=self.tau())
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(linear(o, self.proj))
 
     def forward(self, x, mask=None):
         """Reference signature on pre-partitioned windows (num_windows*B, N, C), no shift mask."""
@@ -159,8 +159,8 @@ class SwinTransformerBlock(nn.Module):
         assert L == math.prod(self.input_resolution), "input feature has wrong size"
         geom = geometry(B, self.input_resolution, self.window_size, self.shift_size)
         a = self.attn.forward_tokens(x.reshape(B * L, C), geom).view(B, L, C)
-        x = x + self.drop_path(self.norm1(a))
-        return x + self.drop_path(self.norm2(self.mlp(x)))
+        x = x + self.drop_path(layer_norm(a, self.norm1))
+        return x + self.drop_path(layer_norm(self.mlp(x), self.norm2))
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads_swin={self.num_heads_swin}, "
@@ -181,7 +181,7 @@ class PatchMerging(nn.Module):
     def forward(self, x):
         assert x.shape[1] == math.prod(self.input_resolution), "input feature has wrong size"
         assert all(r % 2 == 0 for r in self.input_resolution), f"x size {self.input_resolution} are not even."
-        return self.norm(self.reduction(patch_merge_gather(x, self.input_resolution)))
+        return layer_norm(linear(patch_merge_gather(x, self.input_resolution), self.reduction), self.norm)
 
     def extra_repr(self):
         return f"input_resolution={self.input_resolution}, dim={self.dim}"
@@ -270,7 +270,7 @@ class PatchEmbed(nn.Module):
             w, st = self.proj.weight.unsqueeze(2), (1,) + tuple(self.proj.stride)
         y = conv3d_cl(x_cl, w, self.proj.bias, st, 0)
         y = y.reshape(B, -1, self.embed_dim)
-        return self.norm(y) if self.norm is not None else y
+        return layer_norm(y, self.norm) if self.norm is not None else y
 
     def flops(self):
         f = self.num_patches * self.embed_dim * self.in_chans * math.prod(self.patch_size)

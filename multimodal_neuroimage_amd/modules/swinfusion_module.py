@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, window_attention_cross, conv3d_cl
+from ..functional import window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -34,7 +34,7 @@ class Mlp_fusion(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+        return self.drop(linear(self.drop(self.act(linear(x, self.fc1))), self.fc2))
 
 
 def window_partition_fusion(x, window_size):
@@ -93,10 +93,10 @@ class WindowAttention_fusion(nn.Module):
     def forward_tokens(self, x, geom):
         """Fused path: x (rows, C) un-partitioned token rows of geometry `geom` -> (rows, C)."""
         _no_attn_dropout(self)
-        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        qkv = linear(x, self.qkv)
         o = window_attention_self(qkv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                   scale=self.scale)
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(linear(o, self.proj))
 
     def forward(self, x, mask=None):
         """Reference signature: x (num_windows*B, N, C) already partitioned (no shift mask).
@@ -139,11 +139,11 @@ class Cross_WindowAttention(nn.Module):
 
     def forward_tokens(self, x, y, geom):
         _no_attn_dropout(self)
-        q = F.linear(x, self.q.weight, self.q.bias)
-        kv = F.linear(y, self.kv.weight, self.kv.bias)
+        q = linear(x, self.q)
+        kv = linear(y, self.kv)
         o = window_attention_cross(q, kv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                    scale=self.scale)
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(linear(o, self.proj))
 
     def forward(self, x, y, mask=None):
         if mask is not None:
@@ -188,9 +188,9 @@ class SwinTransformerBlock_fusion(nn.Module):
     def forward(self, x, x_size):
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
-        a = self.attn.forward_tokens(self.norm1(x).reshape(B * L, C), geom).view(B, L, C)
+        a = self.attn.forward_tokens(layer_norm(x, self.norm1).reshape(B * L, C), geom).view(B, L, C)
         x = x + self.drop_path(a)
-        return x + self.drop_path(self.mlp(self.norm2(x)))
+        return x + self.drop_path(self.mlp(layer_norm(x, self.norm2)))
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads={self.num_heads}, "
@@ -235,14 +235,14 @@ class Cross_SwinTransformerBlock(nn.Module):
     def forward(self, x, y, x_size):
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
-        xn = self.norm1_A(x).reshape(B * L, C)
-        yn = self.norm1_B(y).reshape(B * L, C)
+        xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
+        yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
         a = self.attn_A.forward_tokens(xn, yn, geom).view(B, L, C)
         b = self.attn_B.forward_tokens(yn, xn, geom).view(B, L, C)
         x = x + self.drop_path_A(a)
-        x = x + self.drop_path_A(self.mlp_A(self.norm2_A(x)))
+        x = x + self.drop_path_A(self.mlp_A(layer_norm(x, self.norm2_A)))
         y = y + self.drop_path_B(b)
-        y = y + self.drop_path_B(self.mlp_B(self.norm2_B(y)))
+        y = y + self.drop_path_B(self.mlp_B(layer_norm(y, self.norm2_B)))
         return x, y
 
     def extra_repr(self):
@@ -264,7 +264,7 @@ class PatchMerging_fusion(nn.Module):
     def forward(self, x):
         assert x.shape[1] == math.prod(self.input_resolution), "input feature has wrong size"
         assert all(r % 2 == 0 for r in self.input_resolution), f"x size {self.input_resolution} are not even."
-        return self.reduction(self.norm(patch_merge_gather(x, self.input_resolution)))
+        return linear(layer_norm(patch_merge_gather(x, self.input_resolution), self.norm), self.reduction)
 
     def extra_repr(self):
         return f"input_resolution={self.input_resolution}, dim={self.dim}"
@@ -434,7 +434,7 @@ class PatchEmbed_fusion(nn.Module):
 
     def forward(self, x):
         x = x.flatten(2).transpose(1, 2)
-        return self.norm(x) if self.norm is not None else x
+        return layer_norm(x, self.norm) if self.norm is not None else x
 
 
 class PatchUnEmbed(nn.Module):

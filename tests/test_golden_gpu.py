@@ -17,6 +17,7 @@ from multimodal_neuroimage_amd.modules import swin_v2_module as V2
 from multimodal_neuroimage_amd.modules import multihead_attention as MH
 from multimodal_neuroimage_amd.modules import crossmodal_transformer as CM
 from multimodal_neuroimage_amd import model as M
+from oracle import model as OM
 
 pytestmark = pytest.mark.gpu
 
@@ -190,7 +191,7 @@ def _model_kwargs(golden, name):
     return meta["kwargs"], meta["params"]
 
 
-def _grad_stats_check(golden, prefix, m, tol):
+def _grad_stats_check(golden, prefix, m, tol, elementwise=True):
     g = golden("models.npz")
     names = list(g[prefix + "gnames"])
     gsum = g[prefix + "gsum"]
@@ -201,11 +202,43 @@ def _grad_stats_check(golden, prefix, m, tol):
         grad = p.grad if p.grad is not None else torch.zeros_like(p)
         key = prefix + "d." + n
         if key in g.files:
-            check(grad, g[key], tol=tol, what=n)
+            if elementwise:   # else: covered against float64 by _oracle_grads_check
+                check(grad, g[key], tol=tol, what=n)
         else:
             nrm = float(grad.double().pow(2).sum().sqrt())
             ref = float(np.sqrt(gsq[i]))
             assert abs(nrm - ref) <= tol * max(ref, 1e-8) + 1e-12, f"{n}: |g| {nrm} vs {ref}"
+
+
+def _oracle_grads_check(golden, prefix, m, ref64, floor=2e-3, factor=4.0):
+    """Parameter gradients vs the float64 oracle run of the same model on the same inputs.
+    Deep Swin-V2 logit_scale / q_bias gradients are sums with heavy cancellation: the reference's
+    own fp32 result (the golden file) is up to 2.4e-3 off float64 on them.  Bar per parameter:
+    max rel err <= max(floor, factor * the reference's own fp32 error) — i.e. never worse than the
+    reference beyond noise, and 2e-3 absolute otherwise."""
+    g = golden("models.npz")
+    for n, p in m.named_parameters():
+        if n not in ref64:
+            continue
+        r = ref64[n]
+        got = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().cpu()
+        scale = max(float(r.abs().max()), 1e-30)
+        err = float((got - r).abs().max()) / scale
+        key = prefix + "d." + n
+        ref_err = float((torch.from_numpy(g[key]).double() - r).abs().max()) / scale if key in g.files else 0.0
+        tol = max(floor, factor * ref_err)
+        assert err <= tol, f"{n}: max rel err vs fp64 {err:.3e} > {tol:.1e} (reference fp32: {ref_err:.1e})"
+
+
+def _oracle64(m, fn, target):
+    p = OM.params_of(m, torch.float64)
+    out = fn(p)
+    torch.nn.functional.binary_cross_entropy_with_logits(out, target.double()).backward()
+    return {k: v.grad for k, v in p.items() if v.grad is not None}
+
+
+SF_CFG = dict(window_size=6, Ex_depths=[6, 6], Fusion_depths=[2, 2, 2], Re_depths=[6, 6], heads=6,
+              resolution=(12, 12), head_patch=7)
 
 
 def test_model_swinfusion(golden, device):
@@ -214,16 +247,20 @@ def test_model_swinfusion(golden, device):
     m = M.SwinFusion(**kw).eval()
     recipe.fill_params(m)
     assert [tuple((k, tuple(s))) for k, s in params] == recipe.param_signature(m)
+    A = torch.from_numpy(recipe.randn(4000, (2, 84, 84)))
+    Bv = torch.from_numpy(recipe.randn(4001, (2, 84, 84)))
+    tgt = torch.tensor([[1.0], [0.0]])
+    ref64 = _oracle64(m, lambda p: OM.swinfusion_logits(p, A.double(), Bv.double(), SF_CFG), tgt)
     m = m.to(device)
-    A = torch.from_numpy(recipe.randn(4000, (2, 84, 84))).to(device).requires_grad_(True)
-    Bv = torch.from_numpy(recipe.randn(4001, (2, 84, 84))).to(device).requires_grad_(True)
+    A, Bv = A.to(device).requires_grad_(True), Bv.to(device).requires_grad_(True)
     out = m(A, Bv)["binary_classification"]
-    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.tensor([[1.0], [0.0]], device=device))
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device))
     loss.backward()
     check(out, g["swinfusion.logits"], tol=1e-3, what="logits")
     check(A.grad, g["swinfusion.dA"], tol=1e-3, what="dA")
     check(Bv.grad, g["swinfusion.dB"], tol=1e-3, what="dB")
-    _grad_stats_check(golden, "swinfusion.", m, 2e-3)
+    _grad_stats_check(golden, "swinfusion.", m, 2e-3, elementwise=False)
+    _oracle_grads_check(golden, "swinfusion.", m, ref64)
 
 
 def test_model_swinv2(golden, device):
@@ -231,15 +268,18 @@ def test_model_swinv2(golden, device):
     kw, params = _model_kwargs(golden, "swinv2")
     m = M.SwinTransformerV2(**kw).eval()
     recipe.fill_params(m)
+    X = torch.from_numpy(recipe.randn(4100, (4, 84, 84)))
+    tgt = torch.tensor([[1.0], [0.0], [1.0], [0.0]])
+    ref64 = _oracle64(m, lambda p: OM.swin_v2_logits(p, "", X.double(), kw["patch_size"], kw["window_size"]), tgt)
     m = m.to(device)
-    X = torch.from_numpy(recipe.randn(4100, (4, 84, 84))).to(device).requires_grad_(True)
+    X = X.to(device).requires_grad_(True)
     out = m(X)[kw["fine_tune_task"]]
-    loss = torch.nn.functional.binary_cross_entropy_with_logits(
-        out, torch.tensor([[1.0], [0.0], [1.0], [0.0]], device=device))
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device))
     loss.backward()
     check(out, g["swinv2.logits"], tol=1e-3, what="logits")
     check(X.grad, g["swinv2.dX"], tol=1e-3, what="dX")
-    _grad_stats_check(golden, "swinv2.", m, 2e-3)
+    _grad_stats_check(golden, "swinv2.", m, 2e-3, elementwise=False)
+    _oracle_grads_check(golden, "swinv2.", m, ref64)
 
 
 def test_model_crossmodal(golden, device):

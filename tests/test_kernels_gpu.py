@@ -197,3 +197,64 @@ def test_conv3d_fwd_bwd_vs_oracle(device, B, sp, Cin, Cout, k, stride, pad, slop
     assert rel_err(out, ref) < TOL
     for a, r in zip(dev, leaves):
         assert rel_err(a.grad, r.grad) < TOL
+
+
+LN = [(1000, 12), (70001, 12), (513, 24), (4099, 48), (300, 96)]
+
+
+@pytest.mark.parametrize("rows,C", LN)
+def test_layernorm_fwd_bwd_vs_torch_fp64(device, rows, C):
+    gen = torch.Generator().manual_seed(rows + C)
+    x = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 3 + 1
+    w = torch.randn(C, generator=gen, dtype=torch.float64)
+    b = torch.randn(C, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    ref = torch.nn.functional.layer_norm(leaves[0], (C,), leaves[1], leaves[2], 1e-5)
+    (ref * g).sum().backward()
+    ln = torch.nn.LayerNorm(C).to(device)
+    with torch.no_grad():
+        ln.weight.copy_(w.float())
+        ln.bias.copy_(b.float())
+    xd = x.float().to(device).requires_grad_(True)
+    out = MF.layer_norm(xd, ln)
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    assert rel_err(xd.grad, leaves[0].grad) < TOL
+    assert rel_err(ln.weight.grad, leaves[1].grad) < TOL
+    assert rel_err(ln.bias.grad, leaves[2].grad) < TOL
+
+
+LIN = [(5000, 12, 36), (4097, 12, 12), (3001, 12, 48), (3001, 48, 12), (2000, 48, 144), (1000, 24, 72), (777, 96, 48)]
+
+
+@pytest.mark.parametrize("rows,K,N", LIN)
+def test_token_linear_weight_grad_vs_torch_fp64(device, rows, K, N):
+    gen = torch.Generator().manual_seed(rows + K * 7 + N)
+    x = torch.randn(rows, K, generator=gen, dtype=torch.float64)
+    w = torch.randn(N, K, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(N, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, N, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    ref = torch.nn.functional.linear(*leaves)
+    (ref * g).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b)]
+    out = MF.linear(dev[0], dev[1], dev[2])
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    for a, r in zip(dev, leaves):
+        assert rel_err(a.grad, r.grad) < TOL
+
+
+def test_token_linear_weight_grad_is_deterministic(device):
+    x = torch.randn(100003, 12, device=device)
+    g = torch.randn(100003, 36, device=device)
+    w = torch.randn(36, 12, device=device, requires_grad=True)
+    grads = []
+    for _ in range(3):
+        w.grad = None
+        (MF.linear(x, w) * g).sum().backward()
+        grads.append(w.grad.clone())
+    assert all(torch.equal(grads[0], gg) for gg in grads[1:])
