@@ -117,15 +117,44 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t rows, const 
     }
 }
 
-// out[j] (+)= sum_b part[b][j], fixed order over b (one thread per output column)
-__global__ void column_sum_kernel(const float* __restrict__ part, int nparts, int ncols, float* __restrict__ out,
-                                  int ld_out, int accumulate) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= ncols) return;
-    double s = 0.0;
-    for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * ncols + j];
-    (void)ld_out;
-    out[j] = accumulate ? out[j] + (float)s : (float)s;
+// out[j] = sum_b part[b][j] in a fixed order (columns j >= split go to out2[j - split]) (deterministic for a given nparts): a block owns CW
+// columns, its 1024 threads split the rows into RG = 1024 / CW interleaved groups with four
+// independent double accumulators each, then the groups are combined in order through LDS.
+template <int CW>
+__global__ __launch_bounds__(1024) void column_sum_kernel(const float* __restrict__ part, int nparts, int ncols,
+                                                          float* __restrict__ out, int split,
+                                                          float* __restrict__ out2) {
+    constexpr int RG = 1024 / CW;
+    __shared__ double red[RG][CW];
+    const int tx = threadIdx.x % CW, ty = threadIdx.x / CW;
+    const int j = blockIdx.x * CW + tx;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    if (j < ncols) {
+        int b = ty;
+        for (; b + 3 * RG < nparts; b += 4 * RG) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] += part[(int64_t)(b + u * RG) * ncols + j];
+        }
+        for (int u = 0; b < nparts; b += RG, ++u) s[u & 3] += part[(int64_t)b * ncols + j];
+    }
+    red[ty][tx] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (ty == 0 && j < ncols) {
+        double t = 0.0;
+        for (int g = 0; g < RG; ++g) t += red[g][tx];
+        if (j < split) out[j] = (float)t;
+        else if (out2) out2[j - split] = (float)t;
+    }
+}
+
+static void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2,
+                       hipStream_t s) {
+    if (ncols <= 16)
+        column_sum_kernel<16><<<(ncols + 15) / 16, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
+    else if (ncols <= 32)
+        column_sum_kernel<32><<<(ncols + 31) / 32, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
+    else
+        column_sum_kernel<64><<<(ncols + 63) / 64, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
 }
 
 using f4 = __attribute__((ext_vector_type(4))) float;
@@ -203,28 +232,37 @@ __global__ __launch_bounds__(256) void linear_dw_kernel(int64_t rows, int N, int
         load_step(st, a0, b0);
         mma_step(a0, b0);
     }
-    // write this wave's partial: part[wave][N*K + N]
-    float* pw = part + (int64_t)wave * (N * K + N);
+    // fold the block's 4 wave tiles in LDS in wave order (deterministic), then write one partial
+    // per block: part[block][N*K + N]
+    extern __shared__ float tile[];   // [N*K + N]
+    const int wib = threadIdx.x >> 6;
+    for (int w = 0; w < 4; ++w) {
+        if (wib == w) {
 #pragma unroll
-    for (int m = 0; m < NT; ++m)
+            for (int m = 0; m < NT; ++m)
 #pragma unroll
-        for (int t = 0; t < KT; ++t)
+                for (int t = 0; t < KT; ++t)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int n = m * 16 + lk * 4 + e;   // C/D row
-                const int k = t * 16 + li;           // C/D col
-                if (n < N && k < K) pw[n * K + k] = acc[m][t][e];
+                    for (int e = 0; e < 4; ++e) {
+                        const int n = m * 16 + lk * 4 + e;   // C/D row
+                        const int k = t * 16 + li;           // C/D col
+                        if (n < N && k < K) tile[n * K + k] = (w ? tile[n * K + k] : 0.f) + acc[m][t][e];
+                    }
+            if (with_bias) {
+#pragma unroll
+                for (int m = 0; m < NT; ++m) {
+                    float v = bsum[m];
+                    v += __shfl_xor(v, 16);
+                    v += __shfl_xor(v, 32);
+                    const int n = m * 16 + li;
+                    if (lk == 0 && n < N) tile[N * K + n] = (w ? tile[N * K + n] : 0.f) + v;
+                }
             }
-    if (with_bias) {
-#pragma unroll
-        for (int m = 0; m < NT; ++m) {
-            float v = bsum[m];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            const int n = m * 16 + li;
-            if (lk == 0 && n < N) pw[N * K + n] = v;
         }
+        __syncthreads();
     }
+    float* pw = part + (int64_t)blockIdx.x * (N * K + N);
+    for (int e = threadIdx.x; e < N * K + N; e += blockDim.x) pw[e] = tile[e];
 }
 
 }  // namespace mmni
@@ -256,7 +294,7 @@ extern "C" int mmni_layernorm_fwd(int64_t rows, int C, const float* x, const flo
 }
 
 extern "C" size_t mmni_layernorm_bwd_workspace_bytes(int64_t rows, int C) {
-    return ((size_t)ln_grid(rows) + 1) * 2 * C * sizeof(float);
+    return (size_t)ln_grid(rows) * 2 * C * sizeof(float);
 }
 
 extern "C" int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const float* x, const float* gamma,
@@ -273,22 +311,14 @@ extern "C" int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const fl
     int rc = launch_status("layernorm_bwd");
     if (rc) return rc;
     // columns [0, C) -> dgamma, [C, 2C) -> dbeta: two fixed-order column sums
-    column_sum_kernel<<<1, 256, 0, (hipStream_t)stream>>>(part, grid, 2 * C, reinterpret_cast<float*>(workspace) +
-                                                                                 (size_t)grid * 2 * C, 0, 0);
-    rc = launch_status("layernorm_colsum");
-    if (rc) return rc;
-    const float* sums = reinterpret_cast<const float*>(workspace) + (size_t)grid * 2 * C;
-    hipError_t e = hipMemcpyAsync(dgamma, sums, C * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(dbeta, sums + C, C * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream);
-    if (e != hipSuccess) { set_error("layernorm_bwd copy: %s", hipGetErrorString(e)); return (int)e; }
-    return 0;
+    column_sum(part, grid, 2 * C, dgamma, C, dbeta, (hipStream_t)stream);   // [0,C) dgamma, [C,2C) dbeta
+    return launch_status("layernorm_colsum");
 }
 
 static int dw_waves() { return 4096; }
 
 extern "C" size_t mmni_linear_dw_workspace_bytes(int N, int K) {
-    return (size_t)dw_waves() * (N * K + N) * sizeof(float) + (size_t)(N * K + N) * sizeof(float);
+    return (size_t)(dw_waves() / 4) * (N * K + N) * sizeof(float);   // per-block partials
 }
 
 extern "C" int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy,
@@ -300,10 +330,12 @@ extern "C" int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_
     const int waves = dw_waves();
     const int grid = waves * 64 / 256;
     const int wb = db != nullptr;
+    const size_t lds = (size_t)(N * K + N) * sizeof(float);
+    MMNI_ARG_CHECK(lds <= 64 * 1024, "linear_dw: N*K too large");
     hipStream_t s = (hipStream_t)stream;
 #define MMNI_DW_CASE(A, B)                                                                     \
     if (NT == A && KT == B) {                                                                  \
-        linear_dw_kernel<A, B><<<grid, 256, 0, s>>>(rows, N, K, x, ldx, dy, lddy, part, wb);    \
+        linear_dw_kernel<A, B><<<grid, 256, lds, s>>>(rows, N, K, x, ldx, dy, lddy, part, wb);    \
     } else
     MMNI_DW_CASE(1, 1) MMNI_DW_CASE(1, 2) MMNI_DW_CASE(1, 3) MMNI_DW_CASE(2, 1) MMNI_DW_CASE(3, 1)
     MMNI_DW_CASE(2, 2) MMNI_DW_CASE(3, 3) MMNI_DW_CASE(1, 4) MMNI_DW_CASE(4, 1) MMNI_DW_CASE(2, 3)
@@ -319,13 +351,8 @@ extern "C" int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_
     int rc = launch_status("linear_dw");
     if (rc) return rc;
     const int cols = N * K + N;
-    float* sums = part + (size_t)waves * cols;
-    column_sum_kernel<<<(cols + 255) / 256, 256, 0, s>>>(part, waves, cols, sums, 0, 0);
+    column_sum(part, waves / 4, cols, dw, N * K, db, s);
     rc = launch_status("linear_dw_colsum");
     if (rc) return rc;
-    hipError_t e = hipMemcpyAsync(dw, sums, (size_t)N * K * sizeof(float), hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess && db)
-        e = hipMemcpyAsync(db, sums + N * K, (size_t)N * sizeof(float), hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) { set_error("linear_dw copy: %s", hipGetErrorString(e)); return (int)e; }
     return 0;
 }

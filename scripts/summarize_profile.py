@@ -29,6 +29,15 @@ def bench_key(name):
     m = re.search(r"mmni::(conv3d_\w+?)_kernel<(\d+), (\d+)", name)
     if m:
         return f"{m.group(1)}_{m.group(2)}x{m.group(3)}"
+    m = re.search(r"mmni::(layernorm_(?:fwd|bwd))_kernel<(\d+)>", name)
+    if m:
+        return f"{m.group(1)}_C{m.group(2)}"
+    m = re.search(r"mmni::linear_dw_kernel<(\d+), (\d+)>", name)
+    if m:
+        return f"linear_dw_tiles{m.group(1)}x{m.group(2)}"
+    m = re.search(r"mmni::(wattn_absmax|wattn_dtable_convert|column_sum)_kernel", name)
+    if m:
+        return m.group(1)
     return None
 
 
