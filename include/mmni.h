@@ -170,6 +170,26 @@ size_t mmni_linear_dw_workspace_bytes(int N, int K);
 int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy,
                    int64_t lddy, float* dw, float* db, void* workspace, void* stream);
 
+/* Token Linear forward / input-gradient (tokenlinear.hip): rows x K -> rows x N, one lane per row,
+ * replacing hipBLASLt on the block Linears (swinfusion_module.py:25-31,104-110,203-205;
+ * swin_v2_module.py:26-32) and fusing their epilogues:
+ *   epi 0  y = x W^T (+ bias)
+ *   epi 1  y = gelu(x W^T + bias)                          (Mlp fc1 + nn.GELU, exact erf)
+ *   epi 2  y = (x W^T) * gelu'(aux W2^T + b2)               (Mlp backward: x = dY of fc2,
+ *          W = fc2.weight^T, aux = fc1 input (rows x K2), W2/b2 = fc1 weight/bias)
+ * W(n, k) = w[n*w_sn + k*w_sk]: (w_sn, w_sk) = (K, 1) for an nn.Linear weight, (1, N) for its
+ * transpose.  x / y / aux rows 16-byte aligned.  Returns -2 for a shape outside the compiled set
+ * (mmni_token_linear_supported). */
+typedef struct mmni_tlin_desc {
+    int64_t rows;
+    int32_t K, N, epi, K2;
+    int64_t ldx, ldy, ldaux;
+    int64_t w_sn, w_sk;
+} mmni_tlin_desc;
+int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const float* w, const float* bias,
+                      const float* aux, const float* w2, const float* b2, float* y, void* stream);
+int mmni_token_linear_supported(int K, int N, int epi, int K2);
+
 int mmni_version(void);
 const char* mmni_last_error(void);
 

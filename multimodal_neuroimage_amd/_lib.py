@@ -43,6 +43,11 @@ class Conv3dDesc(ctypes.Structure):
                 ("Do", _c_i32), ("Ho", _c_i32), ("Wo", _c_i32), ("slope", _c_f)]
 
 
+class TLinDesc(ctypes.Structure):
+    _fields_ = [("rows", _c_i64), ("K", _c_i32), ("N", _c_i32), ("epi", _c_i32), ("K2", _c_i32),
+                ("ldx", _c_i64), ("ldy", _c_i64), ("ldaux", _c_i64), ("w_sn", _c_i64), ("w_sk", _c_i64)]
+
+
 # symbol -> (restype, argtypes); every symbol include/mmni.h declares
 SIGNATURES = {
     "mmni_version": (_c_int, []),
@@ -63,6 +68,8 @@ SIGNATURES = {
     "mmni_layernorm_bwd": (_c_int, [_c_i64, _c_int] + [_vp] * 10),
     "mmni_linear_dw_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int]),
     "mmni_linear_dw": (_c_int, [_c_i64, _c_int, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp]),
+    "mmni_token_linear": (_c_int, [ctypes.POINTER(TLinDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmni_token_linear_supported": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
 }
 
 _lib = None

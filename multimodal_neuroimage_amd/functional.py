@@ -4,8 +4,9 @@ Every op here runs the hand-written HIP kernels; there is no eager/CPU fallback:
 are not float32 ROCm-device tensors raise.  Outputs and saved tensors are allocated by torch
 (caching allocator), the library only launches on torch's current stream.
 """
-from dataclasses import dataclass
+import ctypes
 import math
+from dataclasses import dataclass
 
 import torch
 import torch.nn.functional as F
@@ -439,37 +440,121 @@ _DW_TILES = {(1, 1), (1, 2), (1, 3), (2, 1), (3, 1), (2, 2), (3, 3), (1, 4), (4,
              (4, 4), (6, 6), (4, 12), (12, 4)}
 
 
+def _tlin_ok(K, N, epi=0, K2=0):
+    return bool(_lib.load().mmni_token_linear_supported(K, N, epi, K2))
+
+
+def _tlin(x2, w, bias, K, N, epi=0, transposed=False, aux=None, w2=None, b2=None, K2=0):
+    """HIP token Linear on (rows, K) rows -> (rows, N).  w is an nn.Linear weight (N, K), or
+    with transposed=True the weight (K, N) of the Linear whose input gradient this is."""
+    rows = x2.shape[0]
+    y = torch.empty(rows, N, device=x2.device, dtype=torch.float32)
+    d = _lib.TLinDesc()
+    d.rows, d.K, d.N, d.epi, d.K2 = rows, K, N, epi, K2
+    d.ldx, d.ldy, d.ldaux = x2.stride(0), N, (aux.stride(0) if aux is not None else 0)
+    d.w_sn, d.w_sk = (1, N) if transposed else (K, 1)
+    L = _lib.load()
+    ev = KernelTimer.start()
+    check(L.mmni_token_linear(ctypes.byref(d), ptr(x2), ptr(w), ptr(bias), ptr(aux), ptr(w2), ptr(b2), ptr(y),
+                              stream_handle(x2.device)), "mmni_token_linear")
+    extra = 2.0 * rows * K2 * N if epi == 2 else 0.0
+    KernelTimer.stop(f"token_linear_e{epi}_{K}x{N}", ev, 2.0 * rows * K * N + extra,
+                     4.0 * rows * (K + N + (K2 if epi == 2 else 0)))
+    return y
+
+
+def _rows2d(t, C):
+    t2 = t.reshape(-1, C)
+    return t2 if (t2.stride(1) == 1 and t2.stride(0) % 4 == 0 and t2.data_ptr() % 16 == 0) else t2.contiguous()
+
+
+def _linear_dw(x2, dy2, N, K, with_bias):
+    rows = x2.shape[0]
+    dw = torch.empty(N, K, device=x2.device, dtype=torch.float32)
+    db = torch.empty(N, device=x2.device, dtype=torch.float32) if with_bias else None
+    L = _lib.load()
+    ws = torch.empty(L.mmni_linear_dw_workspace_bytes(N, K) // 4, device=x2.device, dtype=torch.float32)
+    ev = KernelTimer.start()
+    check(L.mmni_linear_dw(rows, N, K, ptr(x2), x2.stride(0), ptr(dy2), dy2.stride(0), ptr(dw), ptr(db), ptr(ws),
+                           stream_handle(x2.device)), "mmni_linear_dw")
+    KernelTimer.stop(f"linear_dw_{N}x{K}", ev, 2.0 * rows * N * K, 4.0 * rows * (N + K))
+    return dw, db
+
+
 class _TokenLinear(torch.autograd.Function):
-    """y = x W^T + b on token rows; forward and dX on hipBLASLt (torch), dW/db on the HIP
-    MFMA reduction (the K = rows weight-gradient GEMM is where the library kernels stall)."""
+    """y = x W^T + b on token rows.  Forward and dX on the HIP token-linear kernel when the shape
+    is compiled (else hipBLASLt via torch), dW/db on the HIP MFMA reduction (the K = rows
+    weight-gradient GEMM is where the library kernels stall)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+        N, K = weight.shape
+        x2 = _rows2d(x, K)
+        ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        ctx.xshape = x.shape
+        if _tlin_ok(K, N):
+            y = _tlin(x2, weight, bias, K, N)
+        else:
+            y = F.linear(x2, weight, bias)
+        return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        x2, weight = ctx.saved_tensors
         N, K = weight.shape
-        x2 = x.reshape(-1, K)
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        dy2 = dy.reshape(-1, N)
-        if not dy2.is_contiguous():
-            dy2 = dy2.contiguous()
-        dx = (dy2 @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
-        rows = x2.shape[0]
-        dw = torch.empty_like(weight)
-        db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
-        L = _lib.load()
-        ws = torch.empty(L.mmni_linear_dw_workspace_bytes(N, K) // 4, device=x.device, dtype=torch.float32)
-        ev = KernelTimer.start()
-        check(L.mmni_linear_dw(rows, N, K, ptr(x2), K, ptr(dy2), N, ptr(dw), ptr(db), ptr(ws),
-                               stream_handle(x.device)), "mmni_linear_dw")
-        KernelTimer.stop(f"linear_dw_{N}x{K}", ev, 2.0 * rows * N * K, 4.0 * rows * (N + K))
+        dy2 = _rows2d(dy, N)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _tlin(dy2, weight, None, N, K, transposed=True) if _tlin_ok(N, K) else dy2 @ weight
+            dx = dx.view(ctx.xshape)
+        dw, db = _linear_dw(x2, dy2, N, K, ctx.has_bias)
         return dx, dw, db
+
+
+class _Mlp(torch.autograd.Function):
+    """fc2(GELU(fc1(x))) on token rows (Mlp / Mlp_fusion, swin_v2_module.py:16-32,
+    swinfusion_module.py:14-30) with the GELU fused into the fc1 kernel and, in backward, into
+    the fc2 input-gradient kernel (the fc1 pre-activation is recomputed there, never stored)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        H, C = w1.shape
+        O = w2.shape[0]
+        x2 = _rows2d(x, C)
+        h = _tlin(x2, w1, b1, C, H, epi=1)
+        y = _tlin(h, w2, b2, H, O)
+        ctx.save_for_backward(x2, h, w1, b1, w2)
+        ctx.xshape = x.shape
+        ctx.has_b = (b1 is not None, b2 is not None)
+        return y.view(*x.shape[:-1], O)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, w1, b1, w2 = ctx.saved_tensors
+        H, C = w1.shape
+        O = w2.shape[0]
+        dy2 = _rows2d(dy, O)
+        dw2, db2 = _linear_dw(h, dy2, O, H, ctx.has_b[1])
+        dpre = _tlin(dy2, w2, None, O, H, epi=2, transposed=True, aux=x2, w2=w1, b2=b1, K2=C)
+        dw1, db1 = _linear_dw(x2, dpre, H, C, ctx.has_b[0])
+        dx = _tlin(dpre, w1, None, H, C, transposed=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2, db2
+
+
+def mlp(x, fc1, fc2, act, drop):
+    """The reference Mlp forward `drop(fc2(drop(act(fc1(x)))))` with the fused HIP path when act is
+    exact nn.GELU, the dropouts are inactive and the shapes are compiled; else per-layer."""
+    require_device(x, what="mlp")
+    H, C = fc1.weight.shape
+    O = fc2.weight.shape[0]
+    fused = (isinstance(act, torch.nn.GELU) and act.approximate == "none"
+             and (drop.p == 0.0 or not drop.training)
+             and _tlin_ok(C, H, 1) and _tlin_ok(O, H, 2, C) and _tlin_ok(H, C) and _tlin_ok(H, O)
+             and ((H + 15) // 16, (C + 15) // 16) in _DW_TILES and ((O + 15) // 16, (H + 15) // 16) in _DW_TILES)
+    if not fused:
+        return drop(linear(drop(act(linear(x, fc1))), fc2))
+    return _Mlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
 
 
 def linear(x, lin_or_weight, bias=None):
@@ -480,6 +565,6 @@ def linear(x, lin_or_weight, bias=None):
         weight = lin_or_weight
     require_device(x, what="linear")
     N, K = weight.shape
-    if ((N + 15) // 16, (K + 15) // 16) not in _DW_TILES:
+    if ((N + 15) // 16, (K + 15) // 16) not in _DW_TILES or K % 4:
         return F.linear(x, weight, bias)
     return _TokenLinear.apply(x, weight, bias)

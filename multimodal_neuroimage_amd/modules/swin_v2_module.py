@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear
+from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear, mlp
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -33,7 +33,7 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(linear(self.drop(self.act(linear(x, self.fc1))), self.fc2))
+        return mlp(x, self.fc1, self.fc2, self.act, self.drop)
 
 
 def window_partition(x, window_size):

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear
+from ..functional import window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -34,7 +34,7 @@ class Mlp_fusion(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(linear(self.drop(self.act(linear(x, self.fc1))), self.fc2))
+        return mlp(x, self.fc1, self.fc2, self.act, self.drop)
 
 
 def window_partition_fusion(x, window_size):

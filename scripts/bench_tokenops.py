@@ -42,4 +42,17 @@ for N, K in [(36, 12), (12, 12), (48, 12), (12, 48)]:
     res[f"dw_{N}x{K}_hip_ms"] = timeit(lambda: torch.autograd.grad(y, (w, b), gy, retain_graph=True))
     res[f"dw_{N}x{K}_torch_ms"] = timeit(lambda: (gy.t() @ xi, gy.sum(0)))
     res[f"dw_{N}x{K}_hbm_floor_ms"] = 4.0 * rows * (N + K) / 8e12 * 1e3
+for K, N in [(12, 36), (12, 48), (48, 12)]:
+    xi = torch.randn(rows, K, device=dev)
+    w = torch.randn(N, K, device=dev)
+    b = torch.randn(N, device=dev)
+    res[f"fwd_{K}x{N}_hip_ms"] = timeit(lambda: MF._tlin(xi, w, b, K, N))
+    res[f"fwd_{K}x{N}_torch_ms"] = timeit(lambda: torch.nn.functional.linear(xi, w, b))
+    res[f"fwd_{K}x{N}_hbm_floor_ms"] = 4.0 * rows * (N + K) / 8e12 * 1e3
+fc1, fc2 = torch.nn.Linear(12, 48).to(dev), torch.nn.Linear(48, 12).to(dev)
+act, drop = torch.nn.GELU(), torch.nn.Dropout(0.0)
+xm = torch.randn(rows, 12, device=dev, requires_grad=True)
+gm = torch.randn(rows, 12, device=dev)
+res["mlp_fwdbwd_hip_ms"] = timeit(lambda: torch.autograd.backward(MF.mlp(xm, fc1, fc2, act, drop), gm))
+res["mlp_fwdbwd_torch_ms"] = timeit(lambda: torch.autograd.backward(fc2(act(fc1(xm))), gm))
 print(json.dumps({k: round(v, 4) for k, v in res.items()}))

@@ -258,3 +258,56 @@ def test_token_linear_weight_grad_is_deterministic(device):
         (MF.linear(x, w) * g).sum().backward()
         grads.append(w.grad.clone())
     assert all(torch.equal(grads[0], gg) for gg in grads[1:])
+
+
+TLIN = [(12, 36), (12, 12), (12, 24), (12, 48), (48, 12), (36, 12), (24, 12)]
+
+
+@pytest.mark.parametrize("K,N", TLIN)
+def test_token_linear_fwd_dx_vs_torch_fp64(device, K, N):
+    """HIP forward (epi 0) and input gradient (transposed weight) of a token Linear."""
+    rows = 70001
+    gen = torch.Generator().manual_seed(K * 100 + N)
+    x = torch.randn(rows, K, generator=gen, dtype=torch.float64)
+    w = torch.randn(N, K, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(N, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, N, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    ref = torch.nn.functional.linear(*leaves)
+    (ref * g).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b)]
+    out = MF.linear(dev[0], dev[1], dev[2])
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    for a, r in zip(dev, leaves):
+        assert rel_err(a.grad, r.grad) < TOL
+
+
+@pytest.mark.parametrize("C,H", [(12, 48)])
+def test_fused_mlp_gelu_vs_torch_fp64(device, C, H):
+    """fc1 + exact GELU + fc2 with the GELU fused forward and backward (pre-activation
+    recomputed in the fc2 input-gradient kernel) vs the float64 torch MLP."""
+    rows = 50003
+    gen = torch.Generator().manual_seed(C + H)
+    x = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    w1 = torch.randn(H, C, generator=gen, dtype=torch.float64) * 0.4
+    b1 = torch.randn(H, generator=gen, dtype=torch.float64) * 0.5
+    w2 = torch.randn(C, H, generator=gen, dtype=torch.float64) * 0.2
+    b2 = torch.randn(C, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    ref = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(*leaves[:3])), *leaves[3:])
+    (ref * g).sum().backward()
+    fc1, fc2 = torch.nn.Linear(C, H).to(device), torch.nn.Linear(H, C).to(device)
+    with torch.no_grad():
+        fc1.weight.copy_(w1.float()); fc1.bias.copy_(b1.float())
+        fc2.weight.copy_(w2.float()); fc2.bias.copy_(b2.float())
+    xd = x.float().to(device).requires_grad_(True)
+    out = MF.mlp(xd, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0))
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    got = [xd.grad, fc1.weight.grad, fc1.bias.grad, fc2.weight.grad, fc2.bias.grad]
+    for a, r in zip(got, leaves):
+        assert rel_err(a, r.grad) < TOL
