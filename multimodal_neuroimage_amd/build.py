@@ -26,8 +26,8 @@ def sources():
 
 def _digest():
     h = hashlib.sha256()
-    for f in sources() + [os.path.join(CSRC, "mmni_common.h"),
-                          os.path.join(HERE, "..", "include", "mmni.h"), __file__]:
+    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    for f in sources() + headers + [os.path.join(HERE, "..", "include", "mmni.h"), __file__]:
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(" ".join(FLAGS).encode())

@@ -27,114 +27,9 @@
 //  * Backward recomputes P from the saved log-sum-exp: pass A (lane = query row) produces
 //    dq and the bias-table gradient (LDS atomics, flushed once per workgroup), pass B
 //    (lane = key row) produces dk and dv.  dq/dk/dv need no cross-window reduction.
-#include "mmni_common.h"
+#include "wattn_common.h"
 
 namespace mmni {
-
-struct WGeom {
-    int B, D, H, W;
-    int wd, wh, ww, sd, sh, sw;
-    int nWd, nWh, nWw;
-    int nwin;   // B * nWd * nWh * nWw
-    int N;      // tokens per window
-    int tw, th; // relative-code strides: (2wh-1)(2ww-1), (2ww-1)
-    int off;    // (wd-1)*tw + (wh-1)*th + (ww-1)
-    int Tsz;    // bias table rows
-};
-
-// Region id of a shifted-frame coordinate (swinfusion_module.py:321-331: slices
-// (0,-ws), (-ws,-s), (-s,None) filled with increasing ids).
-__device__ __host__ __forceinline__ int shift_region(int c, int L, int ws, int s) {
-    return s == 0 ? 0 : (c < L - ws ? 0 : (c < L - s ? 1 : 2));
-}
-
-struct TokenInfo {
-    int64_t row;  // source token row in the (B, D, H, W) tensor
-    int code;     // i*tw + j*th + k  (relative-position code)
-    int rc;       // packed per-axis region ids
-};
-
-__device__ __forceinline__ TokenInfo token_info(const WGeom& g, int w, int t) {
-    int r = w;
-    const int wx = r % g.nWw; r /= g.nWw;
-    const int wy = r % g.nWh; r /= g.nWh;
-    const int wz = r % g.nWd;
-    const int b = r / g.nWd;
-    const int k = t % g.ww;
-    const int r2 = t / g.ww;
-    const int j = r2 % g.wh;
-    const int i = r2 / g.wh;
-    const int cz = wz * g.wd + i, cy = wy * g.wh + j, cx = wx * g.ww + k;
-    int z = cz + g.sd; if (z >= g.D) z -= g.D;
-    int y = cy + g.sh; if (y >= g.H) y -= g.H;
-    int x = cx + g.sw; if (x >= g.W) x -= g.W;
-    TokenInfo ti;
-    ti.row = ((int64_t)(b * g.D + z) * g.H + y) * g.W + x;
-    ti.code = i * g.tw + j * g.th + k;
-    ti.rc = (shift_region(cz, g.D, g.wd, g.sd) * 3 + shift_region(cy, g.H, g.wh, g.sh)) * 3 +
-            shift_region(cx, g.W, g.ww, g.sw);
-    return ti;
-}
-
-struct WAArgs {
-    WGeom g;
-    int KS, WPB, NPAD, ngroups, kind;
-    float scale;
-    int64_t qs, ks, vs, os;
-    const float* q;
-    const float* k;
-    const float* v;
-    const float* table;
-    const float* tau;
-    float* out;
-    float* lse;
-    // backward
-    const float* o;
-    const float* dout;
-    float* dq;
-    float* dk;
-    float* dv;
-    float* dtable;
-    float* dtau;
-    unsigned long long* dtab_fix;   // global int64 fixed-point accumulator (workspace)
-    unsigned int* maxbits;          // workspace tail: max|dout|, max|v| bits (fixed-point scale)
-};
-
-constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
-constexpr float kNormEps = 1e-12f;          // F.normalize eps (swin_v2_module.py:153)
-constexpr int CH = 4;                       // keys per online-softmax chunk
-
-// The bias-table gradient is a scatter-add of N*N*heads values per window into a
-// (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
-// backward on gfx950 (measured: 27.8 ms vs 4.8 ms without the table update at the C3 shape),
-// integer LDS atomics run at full rate.  So the table gradient is accumulated in 64-bit fixed
-// point: exact, order-independent integer adds, i.e. bitwise deterministic, flushed to a global
-// int64 workspace and converted once.  The scale 2^S is picked per call from a proven bound so
-// the sum cannot overflow and keeps the most precision:
-//   |ds| = p |dO.v - delta| <= 2 * HD * max|dout| * max|v|          (delta is a p-average of dO.v)
-//   each query adds at most one ds per (entry, head)  =>  |entry sum| <= T * that bound
-//   S = 62 - ceil(log2(T * bound))
-// A fixed 2^-32 scale with truncation was measured at 20% error on BCE-loss-sized gradients
-// (table grads ~1e-7 made of ~1e4 contributions of ~1e-10); values are rounded to nearest.
-__device__ __forceinline__ int fix_exponent(const unsigned int* maxbits, int hd, long long T) {
-    const double bound = 2.0 * hd * (double)__uint_as_float(maxbits[0]) * (double)__uint_as_float(maxbits[1]) * (double)T;
-    if (!(bound < 1e300)) return 0;       // non-finite inputs: any scale, the result is garbage anyway
-    if (bound <= 0.0) return 150;
-    int ex;
-    frexp(bound, &ex);                    // bound < 2^ex
-    return max(-60, min(150, 62 - ex));
-}
-
-__device__ __forceinline__ unsigned long long to_fixed(float x, float ymul) {
-    // x * 2^S without a slow f32 -> i64 conversion: y = x * 2^(S-32) (exact), then the integer
-    // part of y and its fraction at 2^31 separately
-    const float y = x * ymul;
-    const float yi = truncf(y);
-    const int hi = (int)yi;                                   // |y| < 2^31 by the bound
-    const int lo = __float2int_rn((y - yi) * 2147483648.0f);  // y - yi exact, |.| < 1
-    const long long v = (long long)hi * 4294967296LL + (long long)lo * 2LL;
-    return (unsigned long long)v;
-}
 
 // max|dout| and max|v| for the fixed-point bound (non-negative float bits order as uints)
 __global__ void wattn_absmax_kernel(const float* dout, long long os, const float* v, long long vs, long long T,
@@ -154,63 +49,6 @@ __global__ void wattn_absmax_kernel(const float* dout, long long os, const float
     if ((threadIdx.x & 63) == 0) {
         atomicMax(&maxbits[0], __float_as_uint(md));
         atomicMax(&maxbits[1], __float_as_uint(mv));
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void load_row(float (&dst)[C], const float* src) {
-    if constexpr (C % 4 == 0) {
-#pragma unroll
-        for (int c = 0; c < C; c += 4) {
-            const float4 t = *reinterpret_cast<const float4*>(src + c);
-            dst[c] = t.x; dst[c + 1] = t.y; dst[c + 2] = t.z; dst[c + 3] = t.w;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < C; ++c) dst[c] = src[c];
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void store_row(float* dst, const float (&src)[C]) {
-    if constexpr (C % 4 == 0) {
-#pragma unroll
-        for (int c = 0; c < C; c += 4)
-            *reinterpret_cast<float4*>(dst + c) = make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]);
-    } else {
-#pragma unroll
-        for (int c = 0; c < C; ++c) dst[c] = src[c];
-    }
-}
-
-// Per-head L2 normalisation (F.normalize(dim=-1), eps 1e-12); returns the raw norms.
-template <int C, int HD>
-__device__ __forceinline__ void normalize_heads(float (&x)[C], float (&nrm)[C / HD]) {
-#pragma unroll
-    for (int h = 0; h < C / HD; ++h) {
-        float ss = 0.f;
-#pragma unroll
-        for (int c = 0; c < HD; ++c) ss += x[h * HD + c] * x[h * HD + c];
-        nrm[h] = sqrtf(ss);
-        const float inv = 1.0f / fmaxf(nrm[h], kNormEps);
-#pragma unroll
-        for (int c = 0; c < HD; ++c) x[h * HD + c] *= inv;
-    }
-}
-
-// Backward of y = x / max(||x||, eps) for one head: dx from dy, y and the raw norm.
-template <int HD>
-__device__ __forceinline__ void normalize_bwd(float* dx, const float* dy, const float* y, float nrm) {
-    if (nrm >= kNormEps) {
-        float dot = 0.f;
-#pragma unroll
-        for (int c = 0; c < HD; ++c) dot += y[c] * dy[c];
-        const float inv = 1.0f / nrm;
-#pragma unroll
-        for (int c = 0; c < HD; ++c) dx[c] = (dy[c] - y[c] * dot) * inv;
-    } else {
-#pragma unroll
-        for (int c = 0; c < HD; ++c) dx[c] = dy[c] * (1.0f / kNormEps);
     }
 }
 
@@ -403,7 +241,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
         dtab_s[e] = 0ull;
     }
     if (tid < NH) dtau_s[tid] = 0.f;
-    const float ymul = exp2f((float)(fix_exponent(a.maxbits, HD, (long long)g.nwin * N) - 32));
+    const float ymul = exp2f((float)fix_exponent(a.maxbits, HD));
     float dtr[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) dtr[h] = 0.f;
@@ -477,7 +315,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
             for (int c = 0; c < C; ++c) dqa[c] = 0.f;
             const int cq = code + g.off;
             for (int n = 0; n < nk; ++n) {
-                const int j = p + KS * n;
+                const int j = p * nk + n;   // contiguous key quarters: see wattn_pk.hip pass A
                 const int2 mt = mw[j];
                 const int kcode = mt.x & 0xffff, rcj = mt.x >> 16;
                 const float madd = (rcj == rc ? 0.f : kMask2) + __int_as_float(mt.y);
@@ -643,9 +481,9 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
 }
 
 __global__ void wattn_dtable_convert_kernel(const unsigned long long* fix, const unsigned int* maxbits, int hd,
-                                            long long T, float* dtable, int n) {
+                                            float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dtable[e] += (float)ldexp((double)(long long)fix[e], -fix_exponent(maxbits, hd, T));
+    if (e < n) dtable[e] += (float)ldexp((double)(long long)fix[e], -fix_exponent(maxbits, hd));
 }
 
 // ------------------------------------------------------------------------------------
@@ -730,7 +568,7 @@ static size_t wattn_lds_bytes(bool bwd, int C, int NH, int WPB, int NPAD, int Ts
     return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
 }
 
-static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, WAConfig& cfg) {
+static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, int chunk, WAConfig& cfg) {
     const int N = g.N;
     int KS = N >= 128 ? 4 : (N >= 32 ? 2 : 1);
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
@@ -739,7 +577,7 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, WAConfig& cfg
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (N * KS);
     if (WPB < 1) WPB = 1;
-    const int NPAD = (N + KS * CH - 1) / (KS * CH) * (KS * CH);
+    const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
     const size_t lds = wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz);
     MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
@@ -762,8 +600,13 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, WAConfig& cfg
     return 0;
 }
 
-static int dispatch(const mmni_wattn_desc* d, int HD, void*& kf, void*& kb, int& maxt) {
+static int dispatch(const mmni_wattn_desc* d, int HD, void*& kf, void*& kb, int& maxt, int& chunk) {
     const int C = d->C;
+    chunk = CH;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, kf, kb, maxt)) {
+        chunk = kPkChunk;
+        return 0;
+    }
 #define MMNI_WA_CASE(CC, HH, MT)                         \
     if (C == CC && HD == HH) {                           \
         kf = WAKernels<CC, HH, MT>::fwd(d->kind);        \
@@ -827,10 +670,11 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
                    "wattn_fwd: q/k/v/out must be 16-byte aligned with strides multiple of 4");
     void *kf, *kb;
     int maxt;
-    rc = dispatch(d, HD, kf, kb, maxt);
+    int chunk = CH;
+    rc = dispatch(d, HD, kf, kb, maxt, chunk);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, false, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, false, chunk, cfg);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
@@ -867,10 +711,11 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                    "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
     void *kf, *kb;
     int maxt;
-    rc = dispatch(d, HD, kf, kb, maxt);
+    int chunk = CH;
+    rc = dispatch(d, HD, kf, kb, maxt, chunk);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, true, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, true, chunk, cfg);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
@@ -882,14 +727,14 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     a.maxbits = reinterpret_cast<unsigned int*>(a.dtab_fix + ntab);
     hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8 + 16, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
-    const long long T = (long long)a.g.nwin * a.g.N;
+    const long long T = (long long)a.g.nwin * a.g.N;   // tokens
     wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C, a.maxbits);
     rc = launch_status("wattn_absmax");
     if (rc) return rc;
     void* args[] = {&a};
     e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
-    wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD, T,
+    wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD,
                                                                                      dtable, ntab);
     return launch_status("wattn_dtable_convert");
 }

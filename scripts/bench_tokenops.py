@@ -49,6 +49,11 @@ for K, N in [(12, 36), (12, 48), (48, 12)]:
     res[f"fwd_{K}x{N}_hip_ms"] = timeit(lambda: MF._tlin(xi, w, b, K, N))
     res[f"fwd_{K}x{N}_torch_ms"] = timeit(lambda: torch.nn.functional.linear(xi, w, b))
     res[f"fwd_{K}x{N}_hbm_floor_ms"] = 4.0 * rows * (N + K) / 8e12 * 1e3
+xg = torch.randn(rows, 12, device=dev)
+w1 = torch.randn(48, 12, device=dev)
+b1 = torch.randn(48, device=dev)
+res["fwd_gelu_12x48_hip_ms"] = timeit(lambda: MF._tlin(xg, w1, b1, 12, 48, epi=1))
+res["fwd_gelu_12x48_torch_ms"] = timeit(lambda: torch.nn.functional.gelu(torch.nn.functional.linear(xg, w1, b1)))
 fc1, fc2 = torch.nn.Linear(12, 48).to(dev), torch.nn.Linear(48, 12).to(dev)
 act, drop = torch.nn.GELU(), torch.nn.Dropout(0.0)
 xm = torch.randn(rows, 12, device=dev, requires_grad=True)
