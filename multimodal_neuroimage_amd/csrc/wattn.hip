@@ -600,10 +600,12 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, int chunk, WA
     return 0;
 }
 
-static int dispatch(const mmni_wattn_desc* d, int HD, void*& kf, void*& kb, int& maxt, int& chunk) {
+static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, int& chunk) {
     const int C = d->C;
     chunk = CH;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, kf, kb, maxt)) {
+    int mf = 0, mb = 0;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, kf, kb, mf, mb)) {
+        maxt = bwd ? mb : mf;
         chunk = kPkChunk;
         return 0;
     }
@@ -671,7 +673,7 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     int chunk = CH;
-    rc = dispatch(d, HD, kf, kb, maxt, chunk);
+    rc = dispatch(d, HD, false, kf, kb, maxt, chunk);
     if (rc) return rc;
     WAConfig cfg;
     rc = plan(a.g, d->C, d->heads, maxt, false, chunk, cfg);
@@ -712,7 +714,7 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     int chunk = CH;
-    rc = dispatch(d, HD, kf, kb, maxt, chunk);
+    rc = dispatch(d, HD, true, kf, kb, maxt, chunk);
     if (rc) return rc;
     WAConfig cfg;
     rc = plan(a.g, d->C, d->heads, maxt, true, chunk, cfg);

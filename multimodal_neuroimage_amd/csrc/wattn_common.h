@@ -80,7 +80,7 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 constexpr int kPkChunk = 6;                 // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
-int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt);
+int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the

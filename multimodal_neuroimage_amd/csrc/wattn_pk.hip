@@ -59,7 +59,7 @@ __device__ __forceinline__ void store_pk(float* dst, const f2 (&s)[C / 2]) {
 // forward
 // ------------------------------------------------------------------------------------
 template <int C, int KIND, int MAXT>
-__global__ __launch_bounds__(MAXT) void wattn_fwd_pk_kernel(WAArgs a) {
+__global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAArgs a) {
     constexpr int HD = 2, NH = C / HD, NP = NH / 2;
     static_assert(NH % 2 == 0, "head pairs");
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -515,9 +515,12 @@ static void* pk_bwd(int kind) {
                 : reinterpret_cast<void*>(&wattn_bwd_pk_kernel<C, 0, MAXT>);
 }
 
-int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt) {
-    if (C == 12) { kf = pk_fwd<12, 1024>(kind); kb = pk_bwd<12, 1024>(kind); maxt = 1024; return 1; }
-    if (C == 24) { kf = pk_fwd<24, 512>(kind); kb = pk_bwd<24, 512>(kind); maxt = 512; return 1; }
+// Forward blocks of <= 512 threads (KS = 2 at N = 216): two blocks share a CU, so one block's
+// K/V gather overlaps the other's compute.  The backward's LDS (bias table + its 64-bit
+// gradient) allows one block per CU; it keeps 1024 threads (KS = 4) for occupancy.
+int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b) {
+    if (C == 12) { kf = pk_fwd<12, 512>(kind); kb = pk_bwd<12, 1024>(kind); maxt_f = 512; maxt_b = 1024; return 1; }
+    if (C == 24) { kf = pk_fwd<24, 512>(kind); kb = pk_bwd<24, 512>(kind); maxt_f = 512; maxt_b = 512; return 1; }
     return 0;
 }
 
