@@ -23,6 +23,9 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_kernel<(\d+), (\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(4)}_C{m.group(2)}"
+    m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk_kernel<(\d+), (\d), \d+>", name)
+    if m:
+        return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
     if m:
         return f"{m.group(1)}_hd{m.group(2)}"
