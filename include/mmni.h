@@ -177,6 +177,9 @@ int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, cons
  *   epi 1  y = gelu(x W^T + bias)                          (Mlp fc1 + nn.GELU, exact erf)
  *   epi 2  y = (x W^T) * gelu'(aux W2^T + b2)               (Mlp backward: x = dY of fc2,
  *          W = fc2.weight^T, aux = fc1 input (rows x K2), W2/b2 = fc1 weight/bias)
+ * residual (nullable, epi 0/1, same shape and row stride as y) is added last: the block's
+ * `x + drop_path(proj(...))` / `x + drop_path(mlp(...))` with an inactive drop_path
+ * (swinfusion_module.py:377-378). y may alias residual.
  * W(n, k) = w[n*w_sn + k*w_sk]: (w_sn, w_sk) = (K, 1) for an nn.Linear weight, (1, N) for its
  * transpose.  x / y / aux rows 16-byte aligned.  Returns -2 for a shape outside the compiled set
  * (mmni_token_linear_supported). */
@@ -187,7 +190,8 @@ typedef struct mmni_tlin_desc {
     int64_t w_sn, w_sk;
 } mmni_tlin_desc;
 int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const float* w, const float* bias,
-                      const float* aux, const float* w2, const float* b2, float* y, void* stream);
+                      const float* aux, const float* w2, const float* b2, const float* residual, float* y,
+                      void* stream);
 int mmni_token_linear_supported(int K, int N, int epi, int K2);
 
 int mmni_version(void);

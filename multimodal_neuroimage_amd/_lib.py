@@ -68,7 +68,7 @@ SIGNATURES = {
     "mmni_layernorm_bwd": (_c_int, [_c_i64, _c_int] + [_vp] * 10),
     "mmni_linear_dw_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int]),
     "mmni_linear_dw": (_c_int, [_c_i64, _c_int, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp]),
-    "mmni_token_linear": (_c_int, [ctypes.POINTER(TLinDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmni_token_linear": (_c_int, [ctypes.POINTER(TLinDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmni_token_linear_supported": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
 }
 

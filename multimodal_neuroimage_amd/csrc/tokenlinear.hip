@@ -26,6 +26,7 @@ struct TLinArgs {
     const float* aux;
     const float* w2;   // fc1 weight (N, K2), nn.Linear layout
     const float* b2;
+    const float* res;  // optional residual added in the epilogue (epi 0/1), row stride ldy
     float* y;
 };
 
@@ -128,6 +129,10 @@ __global__ __launch_bounds__(256) void token_linear_kernel(TLinArgs a) {
                 o[0] = acc[0] * gelu_grad(pre[0] + cv.x); o[1] = acc[1] * gelu_grad(pre[1] + cv.y);
                 o[2] = acc[2] * gelu_grad(pre[2] + cv.z); o[3] = acc[3] * gelu_grad(pre[3] + cv.w);
             }
+            if (EPI != 2 && a.res != nullptr) {
+                const float4 rv = *reinterpret_cast<const float4*>(a.res + r * a.ldy + n);
+                o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
+            }
             *reinterpret_cast<float4*>(a.y + r * a.ldy + n) = make_float4(o[0], o[1], o[2], o[3]);
         }
     }
@@ -142,7 +147,8 @@ static bool aligned16(const void* p, int64_t ld) {
 }
 
 extern "C" int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const float* w, const float* bias,
-                                 const float* aux, const float* w2, const float* b2, float* y, void* stream) {
+                                 const float* aux, const float* w2, const float* b2, const float* residual, float* y,
+                                 void* stream) {
     MMNI_ARG_CHECK(d != nullptr && x && w && y, "token_linear: null pointer");
     MMNI_ARG_CHECK(d->rows > 0 && d->K > 0 && d->N > 0, "token_linear: empty shape");
     MMNI_ARG_CHECK(d->epi >= 0 && d->epi <= 2, "token_linear: epi must be 0, 1 or 2");
@@ -156,7 +162,9 @@ extern "C" int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const 
     TLinArgs a{};
     a.rows = d->rows; a.ldx = d->ldx; a.ldy = d->ldy; a.ldaux = d->ldaux;
     a.w_sn = d->w_sn; a.w_sk = d->w_sk;
-    a.x = x; a.w = w; a.bias = bias; a.aux = aux; a.w2 = w2; a.b2 = b2; a.y = y;
+    MMNI_ARG_CHECK(residual == nullptr || (d->epi != 2 && reinterpret_cast<uintptr_t>(residual) % 16 == 0),
+                   "token_linear: residual needs epi 0/1 and 16-byte alignment");
+    a.x = x; a.w = w; a.bias = bias; a.aux = aux; a.w2 = w2; a.b2 = b2; a.res = residual; a.y = y;
     const int64_t blocks = (d->rows + 255) / 256;
     const int grid = (int)(blocks < 4096 ? blocks : 4096);
     hipStream_t s = (hipStream_t)stream;

@@ -444,9 +444,10 @@ def _tlin_ok(K, N, epi=0, K2=0):
     return bool(_lib.load().mmni_token_linear_supported(K, N, epi, K2))
 
 
-def _tlin(x2, w, bias, K, N, epi=0, transposed=False, aux=None, w2=None, b2=None, K2=0):
+def _tlin(x2, w, bias, K, N, epi=0, transposed=False, aux=None, w2=None, b2=None, K2=0, residual=None):
     """HIP token Linear on (rows, K) rows -> (rows, N).  w is an nn.Linear weight (N, K), or
-    with transposed=True the weight (K, N) of the Linear whose input gradient this is."""
+    with transposed=True the weight (K, N) of the Linear whose input gradient this is.
+    residual (rows, N), contiguous, is added in the epilogue."""
     rows = x2.shape[0]
     y = torch.empty(rows, N, device=x2.device, dtype=torch.float32)
     d = _lib.TLinDesc()
@@ -455,8 +456,8 @@ def _tlin(x2, w, bias, K, N, epi=0, transposed=False, aux=None, w2=None, b2=None
     d.w_sn, d.w_sk = (1, N) if transposed else (K, 1)
     L = _lib.load()
     ev = KernelTimer.start()
-    check(L.mmni_token_linear(ctypes.byref(d), ptr(x2), ptr(w), ptr(bias), ptr(aux), ptr(w2), ptr(b2), ptr(y),
-                              stream_handle(x2.device)), "mmni_token_linear")
+    check(L.mmni_token_linear(ctypes.byref(d), ptr(x2), ptr(w), ptr(bias), ptr(aux), ptr(w2), ptr(b2),
+                              ptr(residual), ptr(y), stream_handle(x2.device)), "mmni_token_linear")
     extra = 2.0 * rows * K2 * N if epi == 2 else 0.0
     KernelTimer.stop(f"token_linear_e{epi}_{K}x{N}", ev, 2.0 * rows * K * N + extra,
                      4.0 * rows * (K + N + (K2 if epi == 2 else 0)))
@@ -487,16 +488,19 @@ class _TokenLinear(torch.autograd.Function):
     weight-gradient GEMM is where the library kernels stall)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, residual):
         N, K = weight.shape
         x2 = _rows2d(x, K)
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
+        r2 = residual.reshape(-1, N).contiguous() if residual is not None else None
         if _tlin_ok(K, N):
-            y = _tlin(x2, weight, bias, K, N)
+            y = _tlin(x2, weight, bias, K, N, residual=r2)
         else:
             y = F.linear(x2, weight, bias)
+            if r2 is not None:
+                y = y + r2
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -509,7 +513,7 @@ class _TokenLinear(torch.autograd.Function):
             dx = _tlin(dy2, weight, None, N, K, transposed=True) if _tlin_ok(N, K) else dy2 @ weight
             dx = dx.view(ctx.xshape)
         dw, db = _linear_dw(x2, dy2, N, K, ctx.has_bias)
-        return dx, dw, db
+        return dx, dw, db, (dy if ctx.needs_input_grad[3] else None)
 
 
 class _Mlp(torch.autograd.Function):
@@ -518,12 +522,13 @@ class _Mlp(torch.autograd.Function):
     the fc2 input-gradient kernel (the fc1 pre-activation is recomputed there, never stored)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, residual):
         H, C = w1.shape
         O = w2.shape[0]
         x2 = _rows2d(x, C)
         h = _tlin(x2, w1, b1, C, H, epi=1)
-        y = _tlin(h, w2, b2, H, O)
+        r2 = residual.reshape(-1, O).contiguous() if residual is not None else None
+        y = _tlin(h, w2, b2, H, O, residual=r2)
         ctx.save_for_backward(x2, h, w1, b1, w2)
         ctx.xshape = x.shape
         ctx.has_b = (b1 is not None, b2 is not None)
@@ -539,12 +544,13 @@ class _Mlp(torch.autograd.Function):
         dpre = _tlin(dy2, w2, None, O, H, epi=2, transposed=True, aux=x2, w2=w1, b2=b1, K2=C)
         dw1, db1 = _linear_dw(x2, dpre, H, C, ctx.has_b[0])
         dx = _tlin(dpre, w1, None, H, C, transposed=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1, dw2, db2
+        return dx, dw1, db1, dw2, db2, (dy if ctx.needs_input_grad[5] else None)
 
 
-def mlp(x, fc1, fc2, act, drop):
-    """The reference Mlp forward `drop(fc2(drop(act(fc1(x)))))` with the fused HIP path when act is
-    exact nn.GELU, the dropouts are inactive and the shapes are compiled; else per-layer."""
+def mlp(x, fc1, fc2, act, drop, residual=None):
+    """The reference Mlp forward `drop(fc2(drop(act(fc1(x)))))` (+ residual) with the fused HIP
+    path when act is exact nn.GELU, the dropouts are inactive and the shapes are compiled; else
+    per-layer."""
     require_device(x, what="mlp")
     H, C = fc1.weight.shape
     O = fc2.weight.shape[0]
@@ -553,12 +559,13 @@ def mlp(x, fc1, fc2, act, drop):
              and _tlin_ok(C, H, 1) and _tlin_ok(O, H, 2, C) and _tlin_ok(H, C) and _tlin_ok(H, O)
              and ((H + 15) // 16, (C + 15) // 16) in _DW_TILES and ((O + 15) // 16, (H + 15) // 16) in _DW_TILES)
     if not fused:
-        return drop(linear(drop(act(linear(x, fc1))), fc2))
-    return _Mlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+        y = drop(linear(drop(act(linear(x, fc1))), fc2))
+        return y if residual is None else residual + y
+    return _Mlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, residual)
 
 
-def linear(x, lin_or_weight, bias=None):
-    """Token Linear with the HIP weight-gradient kernel when the tile grid is supported."""
+def linear(x, lin_or_weight, bias=None, residual=None):
+    """Token Linear (+ residual) with the HIP kernels when the shape is compiled."""
     if isinstance(lin_or_weight, torch.nn.Linear):
         weight, bias = lin_or_weight.weight, lin_or_weight.bias
     else:
@@ -566,5 +573,6 @@ def linear(x, lin_or_weight, bias=None):
     require_device(x, what="linear")
     N, K = weight.shape
     if ((N + 15) // 16, (K + 15) // 16) not in _DW_TILES or K % 4:
-        return F.linear(x, weight, bias)
-    return _TokenLinear.apply(x, weight, bias)
+        y = F.linear(x, weight, bias)
+        return y if residual is None else residual + y
+    return _TokenLinear.apply(x, weight, bias, residual)

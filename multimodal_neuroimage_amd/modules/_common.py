@@ -41,6 +41,18 @@ class DropPath(nn.Module):
         return x * mask / keep
 
 
+def inactive(m):
+    """True when module m (DropPath / Dropout / Identity / None) is the identity right now, so a
+    residual add can be fused into the producing kernel's epilogue."""
+    if m is None or isinstance(m, nn.Identity):
+        return True
+    if isinstance(m, DropPath):
+        return m.drop_prob == 0.0 or not m.training
+    if isinstance(m, nn.Dropout):
+        return m.p == 0.0 or not m.training
+    return False
+
+
 def relative_index_buffer(window):
     """relative_position_index of a window (any number of axes), int64 (N, N)."""
     axes = [torch.arange(w) for w in window]

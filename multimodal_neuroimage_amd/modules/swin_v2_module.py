@@ -32,8 +32,8 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden_features, out_features)
         self.drop = nn.Dropout(drop)
 
-    def forward(self, x):
-        return mlp(x, self.fc1, self.fc2, self.act, self.drop)
+    def forward(self, x, residual=None):
+        return mlp(x, self.fc1, self.fc2, self.act, self.drop, residual)
 
 
 def window_partition(x, window_size):

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
 from ..functional import window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp
-from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
+from ._common import (DropPath, inactive, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
 
@@ -33,8 +33,8 @@ class Mlp_fusion(nn.Module):
         self.fc2 = nn.Linear(hidden_features, out_features)
         self.drop = nn.Dropout(drop)
 
-    def forward(self, x):
-        return mlp(x, self.fc1, self.fc2, self.act, self.drop)
+    def forward(self, x, residual=None):
+        return mlp(x, self.fc1, self.fc2, self.act, self.drop, residual)
 
 
 def window_partition_fusion(x, window_size):
@@ -90,13 +90,16 @@ class WindowAttention_fusion(nn.Module):
         trunc_normal_(self.relative_position_bias_table, std=.02)
         self.softmax = nn.Softmax(dim=-1)
 
-    def forward_tokens(self, x, geom):
+    def forward_tokens(self, x, geom, residual=None):
         """Fused path: x (rows, C) un-partitioned token rows of geometry `geom` -> (rows, C)."""
         _no_attn_dropout(self)
         qkv = linear(x, self.qkv)
         o = window_attention_self(qkv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                   scale=self.scale)
-        return self.proj_drop(linear(o, self.proj))
+        if residual is not None and inactive(self.proj_drop):
+            return linear(o, self.proj, residual=residual)
+        out = self.proj_drop(linear(o, self.proj))
+        return out if residual is None else residual + out
 
     def forward(self, x, mask=None):
         """Reference signature: x (num_windows*B, N, C) already partitioned (no shift mask).
@@ -137,13 +140,16 @@ class Cross_WindowAttention(nn.Module):
         trunc_normal_(self.relative_position_bias_table, std=.02)
         self.softmax = nn.Softmax(dim=-1)
 
-    def forward_tokens(self, x, y, geom):
+    def forward_tokens(self, x, y, geom, residual=None):
         _no_attn_dropout(self)
         q = linear(x, self.q)
         kv = linear(y, self.kv)
         o = window_attention_cross(q, kv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                    scale=self.scale)
-        return self.proj_drop(linear(o, self.proj))
+        if residual is not None and inactive(self.proj_drop):
+            return linear(o, self.proj, residual=residual)
+        out = self.proj_drop(linear(o, self.proj))
+        return out if residual is None else residual + out
 
     def forward(self, x, y, mask=None):
         if mask is not None:
@@ -188,8 +194,11 @@ class SwinTransformerBlock_fusion(nn.Module):
     def forward(self, x, x_size):
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
-        a = self.attn.forward_tokens(layer_norm(x, self.norm1).reshape(B * L, C), geom).view(B, L, C)
-        x = x + self.drop_path(a)
+        xn = layer_norm(x, self.norm1).reshape(B * L, C)
+        if inactive(self.drop_path):   # residual adds fused into the proj / fc2 epilogues
+            x = self.attn.forward_tokens(xn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
+            return self.mlp(layer_norm(x, self.norm2), residual=x)
+        x = x + self.drop_path(self.attn.forward_tokens(xn, geom).view(B, L, C))
         return x + self.drop_path(self.mlp(layer_norm(x, self.norm2)))
 
     def extra_repr(self):
@@ -237,6 +246,11 @@ class Cross_SwinTransformerBlock(nn.Module):
         geom = geometry(B, x_size, self.window_size, self.shift_size)
         xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
         yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
+        if inactive(self.drop_path_A) and inactive(self.drop_path_B):   # fused residual adds
+            xa = self.attn_A.forward_tokens(xn, yn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
+            yb = self.attn_B.forward_tokens(yn, xn, geom, residual=y.reshape(B * L, C)).view(B, L, C)
+            return (self.mlp_A(layer_norm(xa, self.norm2_A), residual=xa),
+                    self.mlp_B(layer_norm(yb, self.norm2_B), residual=yb))
         a = self.attn_A.forward_tokens(xn, yn, geom).view(B, L, C)
         b = self.attn_B.forward_tokens(yn, xn, geom).view(B, L, C)
         x = x + self.drop_path_A(a)

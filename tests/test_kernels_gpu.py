@@ -264,24 +264,29 @@ TLIN = [(12, 36), (12, 12), (12, 24), (12, 48), (48, 12), (36, 12), (24, 12)]
 
 
 @pytest.mark.parametrize("K,N", TLIN)
-def test_token_linear_fwd_dx_vs_torch_fp64(device, K, N):
-    """HIP forward (epi 0) and input gradient (transposed weight) of a token Linear."""
+@pytest.mark.parametrize("with_res", [False, True])
+def test_token_linear_fwd_dx_vs_torch_fp64(device, K, N, with_res):
+    """HIP forward (epi 0, optional fused residual) and input gradient (transposed weight) of a
+    token Linear."""
     rows = 70001
     gen = torch.Generator().manual_seed(K * 100 + N)
     x = torch.randn(rows, K, generator=gen, dtype=torch.float64)
     w = torch.randn(N, K, generator=gen, dtype=torch.float64) * 0.3
     b = torch.randn(N, generator=gen, dtype=torch.float64)
     g = torch.randn(rows, N, generator=gen, dtype=torch.float64)
-    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
-    ref = torch.nn.functional.linear(*leaves)
+    res = torch.randn(rows, N, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b, res)]
+    ref = torch.nn.functional.linear(*leaves[:3]) + (leaves[3] if with_res else 0)
     (ref * g).sum().backward()
-    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b)]
-    out = MF.linear(dev[0], dev[1], dev[2])
+    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b, res)]
+    out = MF.linear(dev[0], dev[1], dev[2], residual=dev[3] if with_res else None)
     (out * g.float().to(device)).sum().backward()
     torch.cuda.synchronize()
     assert rel_err(out, ref) < TOL
-    for a, r in zip(dev, leaves):
+    for a, r in zip(dev[:3], leaves[:3]):
         assert rel_err(a.grad, r.grad) < TOL
+    if with_res:
+        assert rel_err(dev[3].grad, leaves[3].grad) < TOL
 
 
 @pytest.mark.parametrize("C,H", [(12, 48)])
@@ -304,10 +309,12 @@ def test_fused_mlp_gelu_vs_torch_fp64(device, C, H):
         fc1.weight.copy_(w1.float()); fc1.bias.copy_(b1.float())
         fc2.weight.copy_(w2.float()); fc2.bias.copy_(b2.float())
     xd = x.float().to(device).requires_grad_(True)
-    out = MF.mlp(xd, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0))
+    rd = torch.zeros(rows, C, device=device, requires_grad=True)
+    out = MF.mlp(xd, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0), residual=rd)
     (out * g.float().to(device)).sum().backward()
     torch.cuda.synchronize()
     assert rel_err(out, ref) < TOL
+    assert rel_err(rd.grad, g) < TOL
     got = [xd.grad, fc1.weight.grad, fc1.bias.grad, fc2.weight.grad, fc2.bias.grad]
     for a, r in zip(got, leaves):
         assert rel_err(a, r.grad) < TOL
