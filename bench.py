@@ -25,7 +25,6 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -113,23 +112,16 @@ def cpu_baseline(size, sample):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+    from multimodal_neuroimage_amd import distributed as D
+    env = D.init_from_env()            # one process per GPU, RCCL ("nccl") when WORLD_SIZE > 1
+    world, rank, device = env.world, env.rank, env.device
     torch.manual_seed(55555555)
 
     from multimodal_neuroimage_amd import model as M
     from multimodal_neuroimage_amd.functional import KernelTimer
 
     kw = model_kwargs(args.size)
-    model = M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device)
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
-                                                          gradient_as_bucket_view=True, static_graph=True)
+    model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank)
     lossf = torch.nn.BCEWithLogitsLoss()
@@ -145,23 +137,18 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier(env)
     torch.cuda.synchronize()
     KernelTimer.reset()
     KernelTimer.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    if world > 1:
-        dist.barrier()
+    D.barrier(env)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     KernelTimer.enabled = False
-    if world > 1:
-        t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, env)
     kern = KernelTimer.summary()
     loss_v = float(loss.item())
 
@@ -200,8 +187,7 @@ def main():
                                      total_ms=round(v["total_ms"], 2)) for k, v in kern.items()},
                     peak_mem_gb=round(torch.cuda.max_memory_allocated(device) / 1e9, 1))
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.shutdown(env)
 
 
 if __name__ == "__main__":
