@@ -561,14 +561,17 @@ struct WAConfig {
     size_t lds;
 };
 
-static size_t wattn_lds_bytes(bool bwd, int C, int NH, int WPB, int NPAD, int Tsz) {
+// dstride: u64 words per table-gradient row (NH, or NH + 1 in the packed kernels)
+static size_t wattn_lds_bytes(bool bwd, int C, int NH, int WPB, int NPAD, int Tsz, int dstride) {
     const size_t T = (size_t)WPB * NPAD;
     if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
     const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
-    return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
+    return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * dstride * 8 + (size_t)NH * 4;
 }
 
-static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, int chunk, WAConfig& cfg) {
+static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg) {
+    const int chunk = packed ? kPkChunk : CH;
+    const int dstride = packed ? NH + 1 : NH;
     const int N = g.N;
     int KS = N >= 128 ? 4 : (N >= 32 ? 2 : 1);
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
@@ -578,8 +581,8 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, int chunk, WA
     int WPB = target / (N * KS);
     if (WPB < 1) WPB = 1;
     const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
-    while (WPB > 1 && wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
-    const size_t lds = wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz);
+    while (WPB > 1 && wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz, dstride) > 160 * 1024) --WPB;
+    const size_t lds = wattn_lds_bytes(bwd, C, NH, WPB, NPAD, g.Tsz, dstride);
     MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
     cfg.KS = KS;
     cfg.WPB = WPB;
@@ -600,13 +603,13 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, int chunk, WA
     return 0;
 }
 
-static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, int& chunk) {
+static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed) {
     const int C = d->C;
-    chunk = CH;
+    packed = false;
     int mf = 0, mb = 0;
     if (HD == 2 && wattn_pk_kernels(C, d->kind, kf, kb, mf, mb)) {
         maxt = bwd ? mb : mf;
-        chunk = kPkChunk;
+        packed = true;
         return 0;
     }
 #define MMNI_WA_CASE(CC, HH, MT)                         \
@@ -672,11 +675,11 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
                    "wattn_fwd: q/k/v/out must be 16-byte aligned with strides multiple of 4");
     void *kf, *kb;
     int maxt;
-    int chunk = CH;
-    rc = dispatch(d, HD, false, kf, kb, maxt, chunk);
+    bool packed = false;
+    rc = dispatch(d, HD, false, kf, kb, maxt, packed);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, false, chunk, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
@@ -713,11 +716,11 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                    "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
     void *kf, *kb;
     int maxt;
-    int chunk = CH;
-    rc = dispatch(d, HD, true, kf, kb, maxt, chunk);
+    bool packed = false;
+    rc = dispatch(d, HD, true, kf, kb, maxt, packed);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, true, chunk, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);

@@ -228,8 +228,11 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     float* rs_s = R + (size_t)T * 2 * C;                  // pass B: [T][2NH] lse2, delta (head order)
     int2* meta_s = reinterpret_cast<int2*>(R + (size_t)T * (2 * C + 2 * NH));
     float* tab_s = reinterpret_cast<float*>(meta_s + T);
+    // table gradient rows padded to an odd stride DS = NH + 1 (u64 words): with stride 6 the
+    // 64-bit atomics of queries 16 entries apart hit the same LDS banks
+    constexpr int DS = NH + 1;
     unsigned long long* dtab_s = reinterpret_cast<unsigned long long*>(tab_s + ((g.Tsz * NH + 1) & ~1));
-    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * NH);
+    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * DS);
 
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -237,10 +240,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     const int wl_c = wl < WPB ? wl : WPB - 1;
     const int lane = tid & 63;
 
-    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
-        tab_s[e] = a.table[e] * kLog2e;
-        dtab_s[e] = 0ull;
-    }
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+    for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0ull;
     if (tid < NH) dtau_s[tid] = 0.f;
     const f2 fscale = splat(exp2f((float)fix_exponent(a.maxbits, HD)));
     f2 dtr[NP];
@@ -328,6 +329,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                 const int kcode = mt.x & 0xffff, rcj = mt.x >> 16;
                 const float madd = (rcj == rc ? 0.f : kMask2) + __int_as_float(mt.y);
                 const int tix = (cq - kcode) * NH;
+                const int dix = (cq - kcode) * DS;
                 const f2* tb = reinterpret_cast<const f2*>(tab_s + tix);
                 const f2* kj = reinterpret_cast<const f2*>(kvw + (size_t)j * 2 * C);
                 const f2* vj = kj + C / 2;
@@ -345,8 +347,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                         dqa[2 * P] = pfma(ds, kj[2 * P], dqa[2 * P]);
                         dqa[2 * P + 1] = pfma(ds, kj[2 * P + 1], dqa[2 * P + 1]);
                         const f2 fx = ds * fscale;
-                        atomicAdd(&dtab_s[tix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
-                        atomicAdd(&dtab_s[tix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
+                        atomicAdd(&dtab_s[dix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
+                        atomicAdd(&dtab_s[dix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
                     } else {
                         f2 sc = tb[P] + (splat(madd) - lse2[P]);
                         sc = pfma(aq[2 * P], kj[2 * P], sc);
@@ -358,8 +360,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                         dqa[2 * P] = pfma(ds, kj[2 * P], dqa[2 * P]);
                         dqa[2 * P + 1] = pfma(ds, kj[2 * P + 1], dqa[2 * P + 1]);
                         const f2 fx = ds * fscale;
-                        atomicAdd(&dtab_s[tix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
-                        atomicAdd(&dtab_s[tix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
+                        atomicAdd(&dtab_s[dix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
+                        atomicAdd(&dtab_s[dix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
                     }
                 }
             }
@@ -498,7 +500,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     }
     __syncthreads();
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
-        const unsigned long long v = dtab_s[e];
+        const unsigned long long v = dtab_s[(e / NH) * DS + e % NH];
         if (v != 0ull) atomicAdd(&a.dtab_fix[e], v);
     }
     if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] / (a.tau[tid] * kLog2e));
