@@ -15,6 +15,12 @@
 // permuted into it when staged, dq/dk/dv/out are permuted back before the store.
 #include "wattn_common.h"
 
+// Kernel ablations for experiments only (scripts/build_variant.sh): bit 0 drops the table-gradient
+// atomics, bit 1 the pass-B loop, bit 2 the pass-A loop.  Product builds use 0.
+#ifndef MMNI_ABL
+#define MMNI_ABL 0
+#endif
+
 namespace mmni {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -53,6 +59,28 @@ __device__ __forceinline__ void store_pk(float* dst, const f2 (&s)[C / 2]) {
 #pragma unroll
     for (int i = 0; i < C / 2; i += 2)
         *reinterpret_cast<float4*>(dst + 2 * i) = make_float4(s[i].x, s[i].y, s[i + 1].x, s[i + 1].y);
+}
+
+// natural row in global memory -> pk float2 array, straight from float4 loads: float4 P of a row
+// holds (h 2P c0, h 2P c1, h 2P+1 c0, h 2P+1 c1), i.e. pk elements 2P = (x, z) and 2P+1 = (y, w).
+// (Going through a float[C] array lets the compiler shuffle the pairs through scratch memory.)
+template <int C>
+__device__ __forceinline__ void load_pk(f2 (&d)[C / 2], const float* src) {
+#pragma unroll
+    for (int P = 0; P < C / 4; ++P) {
+        const float4 t = *reinterpret_cast<const float4*>(src + 4 * P);
+        d[2 * P] = (f2){t.x, t.z};
+        d[2 * P + 1] = (f2){t.y, t.w};
+    }
+}
+
+// pk float2 array -> natural row in global memory, scaled
+template <int C>
+__device__ __forceinline__ void store_nat(float* dst, const f2 (&s)[C / 2], float scale) {
+#pragma unroll
+    for (int P = 0; P < C / 4; ++P)
+        *reinterpret_cast<float4*>(dst + 4 * P) = make_float4(s[2 * P].x * scale, s[2 * P + 1].x * scale,
+                                                              s[2 * P].y * scale, s[2 * P + 1].y * scale);
 }
 
 // ------------------------------------------------------------------------------------
@@ -212,27 +240,79 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
 }
 
 // ------------------------------------------------------------------------------------
-// backward (same two-pass structure and LDS regions as wattn_bwd_kernel)
+// backward
 // ------------------------------------------------------------------------------------
+// Same two-pass flash-style structure as wattn_bwd_kernel (pass A: lane = query row -> dq and
+// the table / tau gradients; pass B: lane = key row -> dk, dv), rewritten for issue efficiency:
+//  * Shift-mask and pad handling only in windows that need it: a window is mask-free unless it
+//    is the last one along a shifted axis (shift_region), i.e. ~82% of the windows of a shifted
+//    96^3 block and all windows of an unshifted one.  The mask-free loop has no region test.
+//  * The fixed-point scale 2^S of the table gradient is folded into dO and delta, so ds comes out
+//    pre-scaled; dq/dk/dv accumulate the scaled values and are multiplied by 2^-S (exact) once.
+//  * dO.v - delta is one fma chain seeded with -delta; the fixed-point rounding is a single
+//    v_cvt_rpi_i32_f32 (round half up).
+//  * The metadata of the next key is prefetched, and the table-gradient atomics of a key are
+//    issued one iteration late, after the next key's LDS reads: LDS operations complete in order,
+//    so an atomic issued ahead of a read would make the read's wait include it.
+__device__ __forceinline__ long long fix_round(float x) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return (long long)r;
+}
+
+// window of a group needs the region test (last window along a shifted axis) or pad keys
+__device__ __forceinline__ bool group_masked(const WGeom& g, int grp, int WPB, int NPAD) {
+    if (NPAD != g.N) return true;
+    for (int w2 = 0; w2 < WPB; ++w2) {
+        int w = grp * WPB + w2;
+        if (w >= g.nwin) return true;
+        const int wx = w % g.nWw; w /= g.nWw;
+        const int wy = w % g.nWh; w /= g.nWh;
+        const int wz = w % g.nWd;
+        if ((g.sw && wx == g.nWw - 1) || (g.sh && wy == g.nWh - 1) || (g.sd && wz == g.nWd - 1)) return true;
+    }
+    return false;
+}
+
+template <int C>
+__device__ __forceinline__ void lds_row(f2 (&d)[C / 2], const float* s) {
+#pragma unroll
+    for (int i = 0; i < C / 2; i += 2) {
+        const float4 t = *reinterpret_cast<const float4*>(s + 2 * i);
+        d[i] = (f2){t.x, t.y};
+        d[i + 1] = (f2){t.z, t.w};
+    }
+}
+
+// table row (NHP floats, NHP % 4 == 0) -> NP float2
+template <int NP, int NHP>
+__device__ __forceinline__ void lds_tab(f2 (&d)[NP], const float* s) {
+    float t[NHP];
+#pragma unroll
+    for (int i = 0; i < NHP; i += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(s + i);
+        t[i] = x.x; t[i + 1] = x.y; t[i + 2] = x.z; t[i + 3] = x.w;
+    }
+#pragma unroll
+    for (int P = 0; P < NP; ++P) d[P] = (f2){t[2 * P], t[2 * P + 1]};
+}
+
 template <int C, int KIND, int MAXT>
 __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     constexpr int HD = 2, NH = C / HD, NP = NH / 2;
+    constexpr int NHP = (NH + 3) & ~3;   // table row stride (float4 reads)
+    constexpr int DS = NH + 1;           // table-gradient row stride in u64 (odd: spreads LDS banks)
     static_assert(NH % 2 == 0, "head pairs");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WGeom& g = a.g;
     const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB;
     const int T = WPB * NPAD;
-    float* R = smem;
-    float* kv_s = R;                                      // pass A: [T][2C] pk k (k-hat), pk v
-    float* qd_s = R;                                      // pass B: [T][2C] pk a2, pk dO
-    float* rs_s = R + (size_t)T * 2 * C;                  // pass B: [T][2NH] lse2, delta (head order)
-    int2* meta_s = reinterpret_cast<int2*>(R + (size_t)T * (2 * C + 2 * NH));
-    float* tab_s = reinterpret_cast<float*>(meta_s + T);
-    // table gradient rows padded to an odd stride DS = NH + 1 (u64 words): with stride 6 the
-    // 64-bit atomics of queries 16 entries apart hit the same LDS banks
-    constexpr int DS = NH + 1;
-    unsigned long long* dtab_s = reinterpret_cast<unsigned long long*>(tab_s + ((g.Tsz * NH + 1) & ~1));
-    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * DS);
+    float* rowb = smem;                                   // [T][2C]: pass A pk k | pk v; pass B pk a2 | pk dOs
+    float* rs_s = smem + (size_t)T * 2 * C;               // [T][2NH]: pass B lse2 | -delta*2^S (pk pairs)
+    int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)T * 2 * NH);
+    float* tab_s = reinterpret_cast<float*>(meta_s + T);  // [Tsz][NHP], log2-domain bias
+    unsigned long long* dtab_s = reinterpret_cast<unsigned long long*>(tab_s + (size_t)g.Tsz * NHP);
+    float* dtau_s = reinterpret_cast<float*>(dtab_s + (size_t)g.Tsz * DS);
 
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -240,19 +320,26 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     const int wl_c = wl < WPB ? wl : WPB - 1;
     const int lane = tid & 63;
 
-    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+    for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
+        const int row = e / NHP, h = e - row * NHP;
+        tab_s[e] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
+    }
     for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0ull;
     if (tid < NH) dtau_s[tid] = 0.f;
-    const f2 fscale = splat(exp2f((float)fix_exponent(a.maxbits, HD)));
+    const int fexp = fix_exponent(a.maxbits, HD);
+    const float fs = exp2f((float)fexp);       // 2^S
+    const float ifs = exp2f((float)-fexp);     // 2^-S (exact)
     f2 dtr[NP];
 #pragma unroll
     for (int P = 0; P < NP; ++P) dtr[P] = splat(0.f);
+    const int nk = NPAD / KS;                  // keys (pass A) / queries (pass B) per lane, even
 
     for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
         const int w = grp * WPB + wl;
         const bool active = (wl < WPB) && (w < g.nwin);
+        const bool masked = group_masked(g, grp, WPB, NPAD);
         const int own = wl_c * NPAD + (active ? t : 0);
-        f2 aq[C / 2], dO[C / 2], lse2[NP], dl[NP];
+        f2 aq[C / 2], dO[C / 2], lse2[NP], ndl[NP];
         int64_t row = 0;
         int code = 0, rc = 0;
         if (active) {
@@ -260,119 +347,137 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
             row = ti.row;
             code = ti.code;
             rc = ti.rc;
-            float qr[C], gr[C], orow[C], dd[NH];
-            load_row<C>(qr, a.q + row * a.qs);
-            if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(qr, nrm); }
-            load_row<C>(gr, a.dout + row * a.os);
-            load_row<C>(orow, a.o + row * a.os);
-#pragma unroll
-            for (int h = 0; h < NH; ++h) {
-                const float t2 = (KIND == 1) ? a.tau[h] * kLog2e : a.scale * kLog2e;
-                qr[2 * h] *= t2;
-                qr[2 * h + 1] *= t2;
-                dd[h] = fmaf(orow[2 * h], gr[2 * h], orow[2 * h + 1] * gr[2 * h + 1]);
+            if constexpr (KIND == 1) {
+                float qr[C], nrm[NH];
+                load_row<C>(qr, a.q + row * a.qs);
+                normalize_heads<C, HD>(qr, nrm);
+                pack_row<C>(aq, qr);
+            } else {
+                load_pk<C>(aq, a.q + row * a.qs);
             }
-            pack_row<C>(aq, qr);
-            pack_row<C>(dO, gr);
+            f2 orow[C / 2];
+            load_pk<C>(dO, a.dout + row * a.os);
+            load_pk<C>(orow, a.o + row * a.os);
 #pragma unroll
             for (int P = 0; P < NP; ++P) {
+                const f2 t2 = (KIND == 1) ? (f2){a.tau[2 * P], a.tau[2 * P + 1]} * kLog2e : splat(a.scale * kLog2e);
+                aq[2 * P] *= t2;
+                aq[2 * P + 1] *= t2;
+                const f2 dd = pfma(orow[2 * P], dO[2 * P], orow[2 * P + 1] * dO[2 * P + 1]);
+                ndl[P] = dd * splat(-fs);
+                dO[2 * P] *= splat(fs);
+                dO[2 * P + 1] *= splat(fs);
                 lse2[P] = (f2){a.lse[row * NH + 2 * P], a.lse[row * NH + 2 * P + 1]} * kLog2e;
-                dl[P] = (f2){dd[2 * P], dd[2 * P + 1]};
             }
         } else {
 #pragma unroll
             for (int i = 0; i < C / 2; ++i) { aq[i] = splat(0.f); dO[i] = splat(0.f); }
 #pragma unroll
-            for (int P = 0; P < NP; ++P) { lse2[P] = splat(INFINITY); dl[P] = splat(0.f); }
+            for (int P = 0; P < NP; ++P) { lse2[P] = splat(INFINITY); ndl[P] = splat(0.f); }
         }
         // ---- stage K/V + metadata (owners write their row; pad rows get neutral values)
         if (active && p == 0) {
-            float kr[C], vr[C];
-            load_row<C>(kr, a.k + row * a.ks);
-            if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
-            load_row<C>(vr, a.v + row * a.vs);
             f2 kp[C / 2], vp[C / 2];
-            pack_row<C>(kp, kr);
-            pack_row<C>(vp, vr);
-            store_pk<C>(kv_s + (size_t)own * 2 * C, kp);
-            store_pk<C>(kv_s + (size_t)own * 2 * C + C, vp);
+            if constexpr (KIND == 1) {
+                float kr[C], nrm[NH];
+                load_row<C>(kr, a.k + row * a.ks);
+                normalize_heads<C, HD>(kr, nrm);
+                pack_row<C>(kp, kr);
+            } else {
+                load_pk<C>(kp, a.k + row * a.ks);
+            }
+            load_pk<C>(vp, a.v + row * a.vs);
+            store_pk<C>(rowb + (size_t)own * 2 * C, kp);
+            store_pk<C>(rowb + (size_t)own * 2 * C + C, vp);
             meta_s[own] = make_int2(code | (rc << 16), 0);
         }
-        for (int e = tid; e < T; e += blockDim.x) {
-            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
-            if (t2 >= N || grp * WPB + w2 >= g.nwin) {
-                float4* z = reinterpret_cast<float4*>(kv_s + (size_t)e * 2 * C);
+        if (masked) {
+            for (int e = tid; e < T; e += blockDim.x) {
+                const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+                if (t2 >= N || grp * WPB + w2 >= g.nwin) {
+                    float4* z = reinterpret_cast<float4*>(rowb + (size_t)e * 2 * C);
 #pragma unroll
-                for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                meta_s[e] = make_int2(0, __float_as_int(-INFINITY));
+                    for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    meta_s[e] = make_int2(0x7fff0000, __float_as_int(-INFINITY));
+                }
             }
         }
         __syncthreads();
         const int2* mw = meta_s + wl_c * NPAD;
-        const int nk = NPAD / KS;
 
         // ================= pass A: lane = query row -> dq, dtable, dtau
         {
-            const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
+            const float* kvw = rowb + (size_t)wl_c * NPAD * 2 * C;
             f2 dqa[C / 2];
 #pragma unroll
             for (int i = 0; i < C / 2; ++i) dqa[i] = splat(0.f);
             const int cq = code + g.off;
-            // key schedule: lane p walks its own contiguous quarter of the keys.  With the
-            // interleaved order (p + KS*n) the 16 queries x 4 keys of a wave-instruction repeat
-            // the same relative offset, i.e. the same table-gradient address, ~3 times: the
-            // 64-bit LDS atomics then serialise.  Keys N/KS apart never share an offset within a
-            // wave's 16 consecutive queries.
-            for (int n = 0; n < nk; ++n) {
-                const int j = p * nk + n;
-                const int2 mt = mw[j];
-                const int kcode = mt.x & 0xffff, rcj = mt.x >> 16;
-                const float madd = (rcj == rc ? 0.f : kMask2) + __int_as_float(mt.y);
-                const int tix = (cq - kcode) * NH;
-                const int dix = (cq - kcode) * DS;
-                const f2* tb = reinterpret_cast<const f2*>(tab_s + tix);
-                const f2* kj = reinterpret_cast<const f2*>(kvw + (size_t)j * 2 * C);
-                const f2* vj = kj + C / 2;
+            // lane p walks its own contiguous slice of the keys (keys N/KS apart never share a
+            // relative offset within a wave's consecutive queries: fewer same-address atomics)
+            const int jb = p * nk;
+            int2 mm = mw[jb];
+            // deferred table-gradient atomics of the previous key (issued after this key's reads)
+            unsigned long long* dtp = dtab_s;
+            long long fx[NH];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) fx[h] = 0;
+            for (int n = 0; n < ((MMNI_ABL & 4) ? 0 : nk); ++n) {
+                const int j = jb + n;
+                const int2 mnext = mw[j + 1];   // prefetch (reads past the slice on the last key: unused)
+                const int tix = cq - (mm.x & 0xffff);
+                f2 tb[NP], kj[C / 2], vj[C / 2];
+                lds_tab<NP, NHP>(tb, tab_s + tix * NHP);
+                lds_row<C>(kj, kvw + (size_t)j * 2 * C);
+                lds_row<C>(vj, kvw + (size_t)j * 2 * C + C);
+#pragma unroll
+                for (int h = 0; h < NH; ++h)
+                    if (!(MMNI_ABL & 1)) atomicAdd(&dtp[h], (unsigned long long)fx[h]);
+                dtp = dtab_s + tix * DS;
+                f2 base[NP];
+                if (masked) {
+                    const float madd = ((mm.x >> 16) == rc ? 0.f : kMask2) + __int_as_float(mm.y);
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - lse2[P]);
+                } else {
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] - lse2[P];
+                }
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
-                    f2 pr;
+                    f2 pr, dsv;
                     if constexpr (KIND == 1) {
                         f2 dot = aq[2 * P] * kj[2 * P];
                         dot = pfma(aq[2 * P + 1], kj[2 * P + 1], dot);
-                        pr = exp2_2(dot + (tb[P] + (splat(madd) - lse2[P])));
-                        f2 dp = dO[2 * P] * vj[2 * P];
-                        dp = pfma(dO[2 * P + 1], vj[2 * P + 1], dp);
-                        const f2 ds = pr * (dp - dl[P]);
-                        dtr[P] = pfma(ds, dot, dtr[P]);
-                        dqa[2 * P] = pfma(ds, kj[2 * P], dqa[2 * P]);
-                        dqa[2 * P + 1] = pfma(ds, kj[2 * P + 1], dqa[2 * P + 1]);
-                        const f2 fx = ds * fscale;
-                        atomicAdd(&dtab_s[dix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
-                        atomicAdd(&dtab_s[dix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
+                        pr = exp2_2(dot + base[P]);
+                        f2 tt = pfma(dO[2 * P], vj[2 * P], ndl[P]);
+                        tt = pfma(dO[2 * P + 1], vj[2 * P + 1], tt);
+                        dsv = pr * tt;
+                        dtr[P] = pfma(dsv, dot, dtr[P]);
                     } else {
-                        f2 sc = tb[P] + (splat(madd) - lse2[P]);
-                        sc = pfma(aq[2 * P], kj[2 * P], sc);
+                        f2 sc = pfma(aq[2 * P], kj[2 * P], base[P]);
                         sc = pfma(aq[2 * P + 1], kj[2 * P + 1], sc);
                         pr = exp2_2(sc);
-                        f2 dp = dO[2 * P] * vj[2 * P];
-                        dp = pfma(dO[2 * P + 1], vj[2 * P + 1], dp);
-                        const f2 ds = pr * (dp - dl[P]);
-                        dqa[2 * P] = pfma(ds, kj[2 * P], dqa[2 * P]);
-                        dqa[2 * P + 1] = pfma(ds, kj[2 * P + 1], dqa[2 * P + 1]);
-                        const f2 fx = ds * fscale;
-                        atomicAdd(&dtab_s[dix + 2 * P], (unsigned long long)(long long)__float2int_rn(fx.x));
-                        atomicAdd(&dtab_s[dix + 2 * P + 1], (unsigned long long)(long long)__float2int_rn(fx.y));
+                        f2 tt = pfma(dO[2 * P], vj[2 * P], ndl[P]);
+                        tt = pfma(dO[2 * P + 1], vj[2 * P + 1], tt);
+                        dsv = pr * tt;
                     }
+                    dqa[2 * P] = pfma(dsv, kj[2 * P], dqa[2 * P]);
+                    dqa[2 * P + 1] = pfma(dsv, kj[2 * P + 1], dqa[2 * P + 1]);
+                    fx[2 * P] = fix_round(dsv.x);
+                    fx[2 * P + 1] = fix_round(dsv.y);
                 }
+                mm = mnext;
             }
+#pragma unroll
+            for (int h = 0; h < NH; ++h) atomicAdd(&dtp[h], (unsigned long long)fx[h]);
             for (int o = 1; o < KS; o <<= 1) {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) dqa[i] += shfl2(dqa[i], o);
             }
             if (active && p == 0) {
-                float dqn[C], dq[C];
-                unpack_row<C>(dqn, dqa);
-                if (KIND == 1) {
+                if constexpr (KIND == 1) {
+                    float dqn[C], dq[C];
+                    unpack_row<C>(dqn, dqa);
                     float qr[C], nrm[NH];
                     load_row<C>(qr, a.q + row * a.qs);
                     normalize_heads<C, HD>(qr, nrm);
@@ -380,79 +485,94 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                     for (int h = 0; h < NH; ++h) {
                         float dy[HD];
 #pragma unroll
-                        for (int c = 0; c < HD; ++c) dy[c] = dqn[h * HD + c] * a.tau[h];
+                        for (int c = 0; c < HD; ++c) dy[c] = dqn[h * HD + c] * (a.tau[h] * ifs);
                         normalize_bwd<HD>(dq + h * HD, dy, qr + h * HD, nrm[h]);
                     }
+                    store_row<C>(a.dq + row * a.qs, dq);
                 } else {
-#pragma unroll
-                    for (int c = 0; c < C; ++c) dq[c] = dqn[c] * a.scale;
+                    store_nat<C>(a.dq + row * a.qs, dqa, a.scale * ifs);
                 }
-                store_row<C>(a.dq + row * a.qs, dq);
             }
         }
         __syncthreads();
-        // ---- restage: pk a2 / pk dO and lse2 / delta rows for pass B
+        // ---- restage: pk a2 / pk dOs and lse2 / -delta*2^S rows for pass B
         if (active && p == 0) {
-            store_pk<C>(qd_s + (size_t)own * 2 * C, aq);
-            store_pk<C>(qd_s + (size_t)own * 2 * C + C, dO);
+            store_pk<C>(rowb + (size_t)own * 2 * C, aq);
+            store_pk<C>(rowb + (size_t)own * 2 * C + C, dO);
             f2* rs = reinterpret_cast<f2*>(rs_s + (size_t)own * 2 * NH);
 #pragma unroll
-            for (int P = 0; P < NP; ++P) { rs[P] = lse2[P]; rs[NP + P] = dl[P]; }
+            for (int P = 0; P < NP; ++P) { rs[P] = lse2[P]; rs[NP + P] = ndl[P]; }
         }
-        for (int e = tid; e < T; e += blockDim.x) {
-            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
-            if (t2 >= N || grp * WPB + w2 >= g.nwin) {
-                float4* z = reinterpret_cast<float4*>(qd_s + (size_t)e * 2 * C);
+        if (masked) {
+            for (int e = tid; e < T; e += blockDim.x) {
+                const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+                if (t2 >= N || grp * WPB + w2 >= g.nwin) {
+                    float4* z = reinterpret_cast<float4*>(rowb + (size_t)e * 2 * C);
 #pragma unroll
-                for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                f2* rs = reinterpret_cast<f2*>(rs_s + (size_t)e * 2 * NH);
+                    for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    f2* rs = reinterpret_cast<f2*>(rs_s + (size_t)e * 2 * NH);
 #pragma unroll
-                for (int P = 0; P < NP; ++P) { rs[P] = splat(INFINITY); rs[NP + P] = splat(0.f); }
+                    for (int P = 0; P < NP; ++P) { rs[P] = splat(INFINITY); rs[NP + P] = splat(0.f); }
+                }
             }
         }
         __syncthreads();
 
         // ================= pass B: lane = key row -> dk, dv
         {
-            const float* qdw = qd_s + (size_t)wl_c * NPAD * 2 * C;
+            const float* qdw = rowb + (size_t)wl_c * NPAD * 2 * C;
             const float* rsw = rs_s + (size_t)wl_c * NPAD * 2 * NH;
             f2 kr[C / 2], vr[C / 2], dka[C / 2], dva[C / 2];
             if (active) {
-                float kn[C], vn[C];
-                load_row<C>(kn, a.k + row * a.ks);
-                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kn, nrm); }
-                load_row<C>(vn, a.v + row * a.vs);
-                pack_row<C>(kr, kn);
-                pack_row<C>(vr, vn);
+                if constexpr (KIND == 1) {
+                    float kn[C], nrm[NH];
+                    load_row<C>(kn, a.k + row * a.ks);
+                    normalize_heads<C, HD>(kn, nrm);
+                    pack_row<C>(kr, kn);
+                } else {
+                    load_pk<C>(kr, a.k + row * a.ks);
+                }
+                load_pk<C>(vr, a.v + row * a.vs);
             } else {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) { kr[i] = splat(0.f); vr[i] = splat(0.f); }
             }
 #pragma unroll
             for (int i = 0; i < C / 2; ++i) { dka[i] = splat(0.f); dva[i] = splat(0.f); }
-            for (int n = 0; n < nk; ++n) {
-                const int i = p + KS * n;
-                const int2 mt = mw[i];
-                const int qcode = mt.x & 0xffff, rci = mt.x >> 16;
-                const float madd = (rci == rc ? 0.f : kMask2) + __int_as_float(mt.y);
-                const f2* tb = reinterpret_cast<const f2*>(tab_s + (qcode - code + g.off) * NH);
-                const f2* ai = reinterpret_cast<const f2*>(qdw + (size_t)i * 2 * C);
-                const f2* gi = ai + C / 2;
+            const int cko = g.off - code;
+            const int ib = p * nk;
+            int2 mm = mw[ib];
+            for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nk); ++n) {
+                const int i = ib + n;
+                const int2 mnext = mw[i + 1];
+                f2 tb[NP], ai[C / 2], gi[C / 2];
+                lds_tab<NP, NHP>(tb, tab_s + ((mm.x & 0xffff) + cko) * NHP);
+                lds_row<C>(ai, qdw + (size_t)i * 2 * C);
+                lds_row<C>(gi, qdw + (size_t)i * 2 * C + C);
                 const f2* rsi = reinterpret_cast<const f2*>(rsw + (size_t)i * 2 * NH);
+                f2 base[NP];
+                if (masked) {
+                    const float madd = ((mm.x >> 16) == rc ? 0.f : kMask2) + __int_as_float(mm.y);
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - rsi[P]);
+                } else {
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] - rsi[P];
+                }
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
-                    f2 sc = tb[P] + (splat(madd) - rsi[P]);
-                    sc = pfma(ai[2 * P], kr[2 * P], sc);
+                    f2 sc = pfma(ai[2 * P], kr[2 * P], base[P]);
                     sc = pfma(ai[2 * P + 1], kr[2 * P + 1], sc);
                     const f2 pr = exp2_2(sc);
-                    f2 dp = gi[2 * P] * vr[2 * P];
-                    dp = pfma(gi[2 * P + 1], vr[2 * P + 1], dp);
-                    const f2 ds = pr * (dp - rsi[NP + P]);
+                    f2 tt = pfma(gi[2 * P], vr[2 * P], rsi[NP + P]);
+                    tt = pfma(gi[2 * P + 1], vr[2 * P + 1], tt);
+                    const f2 dsv = pr * tt;
                     dva[2 * P] = pfma(pr, gi[2 * P], dva[2 * P]);
                     dva[2 * P + 1] = pfma(pr, gi[2 * P + 1], dva[2 * P + 1]);
-                    dka[2 * P] = pfma(ds, ai[2 * P], dka[2 * P]);
-                    dka[2 * P + 1] = pfma(ds, ai[2 * P + 1], dka[2 * P + 1]);
+                    dka[2 * P] = pfma(dsv, ai[2 * P], dka[2 * P]);
+                    dka[2 * P + 1] = pfma(dsv, ai[2 * P + 1], dka[2 * P + 1]);
                 }
+                mm = mnext;
             }
             for (int o = 1; o < KS; o <<= 1) {
 #pragma unroll
@@ -462,10 +582,10 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                 }
             }
             if (active && p == 0) {
-                float dkn[C], dk[C], dv[C];
-                unpack_row<C>(dkn, dka);
-                unpack_row<C>(dv, dva);
-                if (KIND == 1) {
+                store_nat<C>(a.dv + row * a.vs, dva, ifs);
+                if constexpr (KIND == 1) {
+                    float dkn[C], dk[C];
+                    unpack_row<C>(dkn, dka);
                     float kraw[C], nrm[NH];
                     load_row<C>(kraw, a.k + row * a.ks);
                     normalize_heads<C, HD>(kraw, nrm);
@@ -473,15 +593,13 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                     for (int h = 0; h < NH; ++h) {
                         float dy[HD];
 #pragma unroll
-                        for (int c = 0; c < HD; ++c) dy[c] = dkn[h * HD + c] * kLn2;
+                        for (int c = 0; c < HD; ++c) dy[c] = dkn[h * HD + c] * (kLn2 * ifs);
                         normalize_bwd<HD>(dk + h * HD, dy, kraw + h * HD, nrm[h]);
                     }
+                    store_row<C>(a.dk + row * a.ks, dk);
                 } else {
-#pragma unroll
-                    for (int c = 0; c < C; ++c) dk[c] = dkn[c] * kLn2;
+                    store_nat<C>(a.dk + row * a.ks, dka, kLn2 * ifs);
                 }
-                store_row<C>(a.dk + row * a.ks, dk);
-                store_row<C>(a.dv + row * a.vs, dv);
             }
         }
         __syncthreads();
@@ -503,7 +621,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
         const unsigned long long v = dtab_s[(e / NH) * DS + e % NH];
         if (v != 0ull) atomicAdd(&a.dtab_fix[e], v);
     }
-    if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] / (a.tau[tid] * kLog2e));
+    if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] * ifs / (a.tau[tid] * kLog2e));
 }
 
 template <int C, int MAXT>
