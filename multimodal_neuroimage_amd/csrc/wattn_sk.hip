@@ -27,6 +27,8 @@
 // finite and the per-chunk rescale (two v_exp_f32 per head pair) is skipped almost always.
 // Backward: flash-style recompute of P from lse; pass A (lane = query) -> dq and the table
 // gradient (64-bit fixed point LDS atomics, wattn_common.h), pass B (lane = key) -> dk, dv.
+#include <type_traits>
+
 #include "wattn_common.h"
 
 namespace mmni {
@@ -146,106 +148,156 @@ __device__ __forceinline__ long long fix_round(float x) {
 
 constexpr float kLazy = 8.0f;   // log2-domain slack of the lazy softmax max
 
+// x-walk of one row of a window: wrapped x coordinate and region id of column c (uniform)
+__device__ __forceinline__ void col_of(const WGeom& g, const Win& v, int c, int& x, int& rx) {
+    const int cx = v.wx * g.ww + c;
+    x = cx + g.sw;
+    if (x >= g.W) x -= g.W;
+    rx = shift_region(cx, g.W, g.ww, g.sw);
+}
+
+// Unit = (window, quarter of 64 rows, head pair): 64 lanes x 2 heads, walking all N tokens of the
+// window on the other side.  A block holds the nq * NP units of one window, so its waves fetch
+// the same walked rows within a few hundred cycles of each other: scalar-cache hits.
+struct Unit {
+    int w, qt, P;
+};
+
+__device__ __forceinline__ f2 lo2(f4 x) { return (f2){x.x, x.y}; }
+__device__ __forceinline__ f2 hi2(f4 x) { return (f2){x.z, x.w}; }
+// byte-offset addressing: every buffer a launch touches is < 2 GiB (checked on the host), so row
+// offsets are 32-bit SALU products instead of 64-bit multiply chains
+__device__ __forceinline__ f4 sload4(const char* base, uint32_t off) { return *(cf4*)(base + off); }
+__device__ __forceinline__ f2 sload2(const char* base, uint32_t off) { return *(cf2*)(base + off); }
+__device__ __forceinline__ f4 vload4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ f2 vload2(const float* p) { return *reinterpret_cast<const f2*>(p); }
+
+template <bool V>
+using bool_c = std::integral_constant<bool, V>;
+
+// Calls body(row_index, code, region) for every token of window v in window order; the x-row of
+// WW tokens (compile-time, WW > 0) is handed over as one batch: body_row(rows[], codes0, rcs[]).
+template <int WW, typename FR>
+__device__ __forceinline__ void walk_window(const WGeom& g, const Win& v, FR&& body_row) {
+    const int ww = WW ? WW : g.ww;
+    for (int kz = 0; kz < g.wd; ++kz) {
+        const int cz = v.wz * g.wd + kz;
+        int z = cz + g.sd;
+        if (z >= g.D) z -= g.D;
+        const int rz = shift_region(cz, g.D, g.wd, g.sd);
+        for (int ky = 0; ky < g.wh; ++ky) {
+            const int cy = v.wy * g.wh + ky;
+            int y = cy + g.sh;
+            if (y >= g.H) y -= g.H;
+            const int ry = shift_region(cy, g.H, g.wh, g.sh);
+            const int rowb = ((v.b * g.D + z) * g.H + y) * g.W;
+            const int codeb = kz * g.tw + ky * g.th;
+            const int rcb = (rz * 3 + ry) * 3;
+            if constexpr (WW > 0) {
+                int rows[WW], rcs[WW];
+#pragma unroll
+                for (int c = 0; c < WW; ++c) {
+                    int x, rx;
+                    col_of(g, v, c, x, rx);
+                    rows[c] = rowb + x;
+                    rcs[c] = rcb + rx;
+                }
+                body_row(rows, codeb, rcs);
+            } else {
+                for (int c = 0; c < ww; ++c) {
+                    int x, rx;
+                    col_of(g, v, c, x, rx);
+                    int rows[1] = {rowb + x}, rcs[1] = {rcb + rx};
+                    body_row(rows, codeb + c, rcs);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------
-// WW > 0: window x-extent known at compile time (the x walk is unrolled); 0 = runtime.
-template <int C, int KC, int WW>
-__global__ __launch_bounds__(512, 2) void wattn_fwd_sk_kernel(WAArgs a, int nq, int nunits) {
-    constexpr int NH = C / 2, NP = NH / 2;
+// WW > 0: window x-extent known at compile time; the x-row of WW keys is one softmax chunk with
+// all its K rows (then all its V rows) fetched before use.  WW = 0: runtime extent, 1-key chunks.
+template <int NH, int WW>
+__global__ __launch_bounds__(1024) void wattn_fwd_sk_kernel(WAArgs a, int nq, int nunits) {
+    constexpr int NP = NH / 2;
+    constexpr int KC = WW ? WW : 1;
     const WGeom& g = a.g;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wpb = blockDim.x >> 6;
+    const int wpb = blockDim.x >> 6;   // = nq * NP: one block walks one window per iteration
     const f2 L2E = splat(kLog2e);
     const float sl2 = a.scale * kLog2e;
-    for (int u = blockIdx.x * wpb + wave; u < nunits; u += gridDim.x * wpb) {
-        const int w = u / nq, qt = u - w * nq;
-        const Win v = window_of(g, w);
-        const int t = qt * 64 + lane;
+    const uint32_t ks4 = (uint32_t)a.ks * 4, vs4 = (uint32_t)a.vs * 4;
+    for (int w = blockIdx.x; w < g.nwin; w += gridDim.x) {
+        const Unit un = {w, wave / NP, wave % NP};
+        const Win v = window_of(g, un.w);
+        const int t = un.qt * 64 + lane;
         const bool act = t < g.N;
-        const TokenInfo ti = token_info(g, w, act ? t : g.N - 1);
+        const TokenInfo ti = token_info(g, un.w, act ? t : g.N - 1);
         const int cq = ti.code + g.off, rq = ti.rc;
-        f2 aq[C / 2];
-        vload_row<C>(aq, a.q + ti.row * a.qs);
-#pragma unroll
-        for (int i = 0; i < C / 2; ++i) aq[i] *= splat(sl2);
-        f2 m[NP], m8[NP], l[NP], acc[C / 2];
-#pragma unroll
-        for (int P = 0; P < NP; ++P) { m[P] = splat(-INFINITY); m8[P] = splat(-INFINITY); l[P] = splat(0.f); }
-#pragma unroll
-        for (int i = 0; i < C / 2; ++i) acc[i] = splat(0.f);
-
-        walk_rows(g, v, [&](int64_t rowb, int codeb, int rcb) {
-            const int ww = WW ? WW : g.ww;
-#pragma unroll
-            for (int kx0 = 0; kx0 < ww; kx0 += KC) {
-                f2 s[KC][NP];
-                int64_t krow[KC];
+        const f4 q4 = vload4(a.q + ti.row * a.qs + 4 * un.P);
+        const f2 aq0 = lo2(q4) * splat(sl2), aq1 = hi2(q4) * splat(sl2);
+        const float* tabP = a.table + 2 * un.P;
+        const char* kP = reinterpret_cast<const char*>(a.k + 4 * un.P);
+        const char* vP = reinterpret_cast<const char*>(a.v + 4 * un.P);
+        f2 m = splat(-INFINITY), m8 = splat(-INFINITY), l = splat(0.f), acc0 = splat(0.f), acc1 = splat(0.f);
+        auto run = [&](auto masked_c) {
+            constexpr bool MASKED = decltype(masked_c)::value;
+            walk_window<WW>(g, v, [&](const int (&rows)[KC], int code0, const int (&rcs)[KC]) {
+                f4 kk[KC];
+                f2 tb[KC];
+                const float* tp = tabP + (cq - code0) * NH;   // bias rows of this x-row: tp - c*NH
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-                    int code, rc;
-                    const int kx = kx0 + c < ww ? kx0 + c : ww - 1;
-                    key_of(g, v, rowb, codeb, rcb, kx, krow[c], code, rc);
-                    f2 kk[C / 2], tb[NP];
-                    sload_row<C>(kk, a.k + krow[c] * a.ks);
-                    vload_tab<NP>(tb, a.table + (cq - code) * NH);
-                    float madd = 0.f;
-                    if (v.masked) madd = rc == rq ? 0.f : kMask2;
-                    if (kx0 + c >= ww) madd = -INFINITY;
-#pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        f2 sc = pfma(tb[P], L2E, splat(madd));
-                        sc = pfma(aq[2 * P], kk[2 * P], sc);
-                        s[c][P] = pfma(aq[2 * P + 1], kk[2 * P + 1], sc);
-                    }
+                    kk[c] = sload4(kP, (uint32_t)rows[c] * ks4);
+                    tb[c] = vload2(tp - c * NH);
                 }
-                // lazy online max: rescale only when a score passes m + 8
-                f2 cm[NP];
-                bool need = false;
-#pragma unroll
-                for (int P = 0; P < NP; ++P) {
-                    cm[P] = s[0][P];
-#pragma unroll
-                    for (int c = 1; c < KC; ++c) cm[P] = (f2){fmaxf(cm[P].x, s[c][P].x), fmaxf(cm[P].y, s[c][P].y)};
-                    need |= (cm[P].x > m8[P].x) | (cm[P].y > m8[P].y);
-                }
-                if (__any(need)) {
-#pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        const f2 mn = (f2){fmaxf(m[P].x, cm[P].x), fmaxf(m[P].y, cm[P].y)};
-                        const f2 al = exp2_2(m[P] - mn);
-                        l[P] *= al;
-                        acc[2 * P] *= al;
-                        acc[2 * P + 1] *= al;
-                        m[P] = mn;
-                        m8[P] = mn + splat(kLazy);
-                    }
-                }
+                f2 s[KC];
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-                    f2 vv[C / 2];
-                    sload_row<C>(vv, a.v + krow[c] * a.vs);
-#pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        const f2 pj = exp2_2(s[c][P] - m[P]);
-                        l[P] += pj;
-                        acc[2 * P] = pfma(pj, vv[2 * P], acc[2 * P]);
-                        acc[2 * P + 1] = pfma(pj, vv[2 * P + 1], acc[2 * P + 1]);
-                    }
+                    f2 sc;
+                    if constexpr (MASKED) sc = pfma(tb[c], L2E, splat(rcs[c] != rq ? kMask2 : 0.f));
+                    else sc = tb[c] * L2E;
+                    sc = pfma(aq0, lo2(kk[c]), sc);
+                    s[c] = pfma(aq1, hi2(kk[c]), sc);
                 }
-            }
-        });
+                // lazy online max: rescale only when a score passes m + 8 (log2 domain)
+                f2 cm = s[0];
+#pragma unroll
+                for (int c = 1; c < KC; ++c) cm = (f2){fmaxf(cm.x, s[c].x), fmaxf(cm.y, s[c].y)};
+                if (__any((cm.x > m8.x) | (cm.y > m8.y))) {
+                    const f2 mn = (f2){fmaxf(m.x, cm.x), fmaxf(m.y, cm.y)};
+                    const f2 al = exp2_2(m - mn);
+                    l *= al;
+                    acc0 *= al;
+                    acc1 *= al;
+                    m = mn;
+                    m8 = mn + splat(kLazy);
+                }
+                f4 vv[KC];
+#pragma unroll
+                for (int c = 0; c < KC; ++c) vv[c] = sload4(vP, (uint32_t)rows[c] * vs4);
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    const f2 pj = exp2_2(s[c] - m);
+                    l += pj;
+                    acc0 = pfma(pj, lo2(vv[c]), acc0);
+                    acc1 = pfma(pj, hi2(vv[c]), acc1);
+                }
+            });
+        };
+        if (v.masked) run(bool_c<true>{});
+        else run(bool_c<false>{});
         if (act) {
-#pragma unroll
-            for (int P = 0; P < NP; ++P) {
-                const f2 inv = (f2){1.0f / l[P].x, 1.0f / l[P].y};
-                acc[2 * P] *= inv;
-                acc[2 * P + 1] *= inv;
-                const f2 lse2 = m[P] + (f2){fast_log2(l[P].x), fast_log2(l[P].y)};
-                *reinterpret_cast<float2*>(a.lse + ti.row * NH + 2 * P) = make_float2(lse2.x, lse2.y);
-            }
-            vstore_row<C>(a.out + ti.row * a.os, acc, 1.0f);
+            const f2 inv = (f2){1.0f / l.x, 1.0f / l.y};
+            acc0 *= inv;
+            acc1 *= inv;
+            *reinterpret_cast<f4*>(a.out + ti.row * a.os + 4 * un.P) = (f4){acc0.x, acc0.y, acc1.x, acc1.y};
+            const f2 lse2 = m + (f2){fast_log2(l.x), fast_log2(l.y)};
+            *reinterpret_cast<f2*>(a.lse + ti.row * NH + 2 * un.P) = lse2;
         }
     }
 }
@@ -260,19 +312,14 @@ __global__ void wattn_prep_sk_kernel(const float* o, const float* dout, int64_t 
     constexpr int NH = C / 2, NP = NH / 2;
     float md = 0.f, mv = 0.f;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < T; r += (int64_t)gridDim.x * blockDim.x) {
-        f2 orow[C / 2], grow[C / 2], vrow[C / 2];
-        vload_row<C>(orow, o + r * os);
-        vload_row<C>(grow, dout + r * os);
-        vload_row<C>(vrow, vv + r * vs);
 #pragma unroll
         for (int P = 0; P < NP; ++P) {
-            const f2 d = pfma(orow[2 * P], grow[2 * P], orow[2 * P + 1] * grow[2 * P + 1]);
-            *reinterpret_cast<float2*>(delta + r * NH + 2 * P) = make_float2(d.x, d.y);
-        }
-#pragma unroll
-        for (int i = 0; i < C / 2; ++i) {
-            md = fmaxf(md, fmaxf(fabsf(grow[i].x), fabsf(grow[i].y)));
-            mv = fmaxf(mv, fmaxf(fabsf(vrow[i].x), fabsf(vrow[i].y)));
+            const f4 o4 = vload4(o + r * os + 4 * P), g4 = vload4(dout + r * os + 4 * P);
+            const f4 v4 = vload4(vv + r * vs + 4 * P);
+            const f2 d = pfma(lo2(o4), lo2(g4), hi2(o4) * hi2(g4));
+            *reinterpret_cast<f2*>(delta + r * NH + 2 * P) = d;
+            md = fmaxf(md, fmaxf(fmaxf(fabsf(g4.x), fabsf(g4.y)), fmaxf(fabsf(g4.z), fabsf(g4.w))));
+            mv = fmaxf(mv, fmaxf(fmaxf(fabsf(v4.x), fabsf(v4.y)), fmaxf(fabsf(v4.z), fabsf(v4.w))));
         }
     }
     for (int o2 = 32; o2 > 0; o2 >>= 1) {
@@ -285,136 +332,83 @@ __global__ void wattn_prep_sk_kernel(const float* o, const float* dout, int64_t 
     }
 }
 
-template <int C, int WW>
-__global__ __launch_bounds__(512, 2) void wattn_bwd_sk_kernel(WAArgs a, int nq, int nunits, const float* delta) {
-    constexpr int NH = C / 2, NP = NH / 2;
+// pass A: lane = query row -> dq and the bias-table gradient
+template <int NH, int WW>
+__global__ __launch_bounds__(1024) void wattn_bwdq_sk_kernel(WAArgs a, int nq, int nunits, const float* delta) {
+    constexpr int NP = NH / 2;
+    constexpr int KC = WW ? WW : 1;
     constexpr int DS = NH + 1;   // odd u64 stride of the table-gradient rows (spreads LDS banks)
     extern __shared__ __attribute__((aligned(16))) unsigned long long dtab_s[];   // [Tsz][DS]
     const WGeom& g = a.g;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wpb = blockDim.x >> 6;
+    const int wpb = blockDim.x >> 6;   // = nq * NP: one block walks one window per iteration
     const f2 L2E = splat(kLog2e);
     const float sl2 = a.scale * kLog2e;
+    const uint32_t ks4 = (uint32_t)a.ks * 4, vs4 = (uint32_t)a.vs * 4;
     for (int e = threadIdx.x; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0ull;
     const int fexp = fix_exponent(a.maxbits, 2);
-    const float fs = exp2f((float)fexp);     // 2^S: ds * 2^S < 2^30 (wattn_common.h)
+    const float fs = exp2f((float)fexp);     // 2^S: |ds| * 2^S < 2^30 (wattn_common.h)
     const float ifs = exp2f((float)-fexp);
     __syncthreads();
 
-    for (int u = blockIdx.x * wpb + wave; u < nunits; u += gridDim.x * wpb) {
-        const int w = u / nq, qt = u - w * nq;
-        const Win v = window_of(g, w);
-        const int t = qt * 64 + lane;
+    for (int w = blockIdx.x; w < g.nwin; w += gridDim.x) {
+        const Unit un = {w, wave / NP, wave % NP};
+        const Win v = window_of(g, un.w);
+        const int t = un.qt * 64 + lane;
         const bool act = t < g.N;
-        const TokenInfo ti = token_info(g, w, act ? t : g.N - 1);
-
-        // ================= pass A: lane = query row -> dq, dtable
-        {
-            f2 aq[C / 2], dOs[C / 2], nlse[NP], ndl[NP], dqa[C / 2];
-            vload_row<C>(aq, a.q + ti.row * a.qs);
-            vload_row<C>(dOs, a.dout + ti.row * a.os);
-            vload_tab<NP>(nlse, a.lse + ti.row * NH);
-            vload_tab<NP>(ndl, delta + ti.row * NH);
+        const TokenInfo ti = token_info(g, un.w, act ? t : g.N - 1);
+        const f4 q4 = vload4(a.q + ti.row * a.qs + 4 * un.P);
+        const f4 g4 = vload4(a.dout + ti.row * a.os + 4 * un.P);
+        const f2 aq0 = lo2(q4) * splat(sl2), aq1 = hi2(q4) * splat(sl2);
+        const float gs = act ? fs : 0.f;
+        const f2 dO0 = lo2(g4) * splat(gs), dO1 = hi2(g4) * splat(gs);
+        const f2 nlse = act ? -vload2(a.lse + ti.row * NH + 2 * un.P) : splat(-INFINITY);
+        const f2 ndl = vload2(delta + ti.row * NH + 2 * un.P) * splat(-gs);
+        const int cq = ti.code + g.off, rq = ti.rc;
+        const float* tabP = a.table + 2 * un.P;
+        const char* kP = reinterpret_cast<const char*>(a.k + 4 * un.P);
+        const char* vP = reinterpret_cast<const char*>(a.v + 4 * un.P);
+        unsigned long long* dtP = dtab_s + 2 * un.P;
+        f2 dq0 = splat(0.f), dq1 = splat(0.f);
+        auto run = [&](auto masked_c) {
+            constexpr bool MASKED = decltype(masked_c)::value;
+            walk_window<WW>(g, v, [&](const int (&rows)[KC], int code0, const int (&rcs)[KC]) {
+                f4 kk[KC], vk[KC];
+                f2 tb[KC];
+                const float* tp = tabP + (cq - code0) * NH;   // bias rows of this x-row: tp - c*NH
+                unsigned long long* dtr = dtP + (cq - code0) * DS;
 #pragma unroll
-            for (int i = 0; i < C / 2; ++i) {
-                aq[i] *= splat(sl2);
-                dOs[i] *= splat(act ? fs : 0.f);
-                dqa[i] = splat(0.f);
-            }
+                for (int c = 0; c < KC; ++c) {
+                    kk[c] = sload4(kP, (uint32_t)rows[c] * ks4);
+                    vk[c] = sload4(vP, (uint32_t)rows[c] * vs4);
+                    tb[c] = vload2(tp - c * NH);
+                }
 #pragma unroll
-            for (int P = 0; P < NP; ++P) {
-                nlse[P] = act ? -nlse[P] : splat(-INFINITY);
-                ndl[P] *= splat(act ? -fs : 0.f);
-            }
-            const int cq = ti.code + g.off, rq = ti.rc;
-            walk_rows(g, v, [&](int64_t rowb, int codeb, int rcb) {
-#pragma unroll
-                for (int kx = 0; kx < (WW ? WW : g.ww); ++kx) {
-                    int64_t row;
-                    int code, rc;
-                    key_of(g, v, rowb, codeb, rcb, kx, row, code, rc);
-                    f2 kk[C / 2], vk[C / 2], tb[NP];
-                    sload_row<C>(kk, a.k + row * a.ks);
-                    sload_row<C>(vk, a.v + row * a.vs);
-                    const int tix = cq - code;
-                    vload_tab<NP>(tb, a.table + tix * NH);
-                    f2 base[NP];
-                    if (v.masked) {
-                        const float madd = rc == rq ? 0.f : kMask2;
-#pragma unroll
-                        for (int P = 0; P < NP; ++P) base[P] = pfma(tb[P], L2E, nlse[P] + splat(madd));
-                    } else {
-#pragma unroll
-                        for (int P = 0; P < NP; ++P) base[P] = pfma(tb[P], L2E, nlse[P]);
-                    }
-                    long long fx[NH];
-#pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        f2 sc = pfma(aq[2 * P], kk[2 * P], base[P]);
-                        sc = pfma(aq[2 * P + 1], kk[2 * P + 1], sc);
-                        const f2 pr = exp2_2(sc);
-                        f2 tt = pfma(dOs[2 * P], vk[2 * P], ndl[P]);
-                        tt = pfma(dOs[2 * P + 1], vk[2 * P + 1], tt);
-                        const f2 dsv = pr * tt;
-                        dqa[2 * P] = pfma(dsv, kk[2 * P], dqa[2 * P]);
-                        dqa[2 * P + 1] = pfma(dsv, kk[2 * P + 1], dqa[2 * P + 1]);
-                        fx[2 * P] = fix_round(dsv.x);
-                        fx[2 * P + 1] = fix_round(dsv.y);
-                    }
-                    unsigned long long* dt = dtab_s + tix * DS;
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) atomicAdd(&dt[h], (unsigned long long)fx[h]);
+                for (int c = 0; c < KC; ++c) {
+                    f2 sc;
+                    if constexpr (MASKED) sc = pfma(tb[c], L2E, nlse + splat(rcs[c] != rq ? kMask2 : 0.f));
+                    else sc = pfma(tb[c], L2E, nlse);
+                    sc = pfma(aq0, lo2(kk[c]), sc);
+                    sc = pfma(aq1, hi2(kk[c]), sc);
+                    const f2 pr = exp2_2(sc);
+                    f2 tt = pfma(dO0, lo2(vk[c]), ndl);
+                    tt = pfma(dO1, hi2(vk[c]), tt);
+                    const f2 dsv = pr * tt;
+                    dq0 = pfma(dsv, lo2(kk[c]), dq0);
+                    dq1 = pfma(dsv, hi2(kk[c]), dq1);
+                    unsigned long long* dt = dtr - c * DS;
+                    atomicAdd(&dt[0], (unsigned long long)fix_round(dsv.x));
+                    atomicAdd(&dt[1], (unsigned long long)fix_round(dsv.y));
                 }
             });
-            if (act) vstore_row<C>(a.dq + ti.row * a.qs, dqa, a.scale * ifs);
-        }
-
-        // ================= pass B: lane = key row -> dk, dv
-        {
-            f2 kr[C / 2], vr[C / 2], dka[C / 2], dva[C / 2];
-            vload_row<C>(kr, a.k + ti.row * a.ks);
-            vload_row<C>(vr, a.v + ti.row * a.vs);
-#pragma unroll
-            for (int i = 0; i < C / 2; ++i) {
-                kr[i] *= splat(sl2);
-                dka[i] = splat(0.f);
-                dva[i] = splat(0.f);
-            }
-            const int cko = g.off - ti.code, rk = ti.rc;
-            walk_rows(g, v, [&](int64_t rowb, int codeb, int rcb) {
-#pragma unroll
-                for (int qx = 0; qx < (WW ? WW : g.ww); ++qx) {
-                    int64_t row;
-                    int code, rc;
-                    key_of(g, v, rowb, codeb, rcb, qx, row, code, rc);
-                    f2 qq[C / 2], gg[C / 2], ll[NP], dd[NP], tb[NP];
-                    sload_row<C>(qq, a.q + row * a.qs);
-                    sload_row<C>(gg, a.dout + row * a.os);
-                    sload_pairs<NP>(ll, a.lse + row * NH);
-                    sload_pairs<NP>(dd, delta + row * NH);
-                    vload_tab<NP>(tb, a.table + (code + cko) * NH);
-                    const float madd = (v.masked && rc != rk) ? kMask2 : 0.f;
-#pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        f2 base = pfma(tb[P], L2E, -ll[P]);
-                        if (v.masked) base += splat(madd);
-                        f2 sc = pfma(qq[2 * P], kr[2 * P], base);
-                        sc = pfma(qq[2 * P + 1], kr[2 * P + 1], sc);
-                        const f2 pr = exp2_2(sc);
-                        f2 tt = pfma(gg[2 * P], vr[2 * P], gg[2 * P + 1] * vr[2 * P + 1]);
-                        const f2 dsv = pr * (tt - dd[P]);
-                        dva[2 * P] = pfma(pr, gg[2 * P], dva[2 * P]);
-                        dva[2 * P + 1] = pfma(pr, gg[2 * P + 1], dva[2 * P + 1]);
-                        dka[2 * P] = pfma(dsv, qq[2 * P], dka[2 * P]);
-                        dka[2 * P + 1] = pfma(dsv, qq[2 * P + 1], dka[2 * P + 1]);
-                    }
-                }
-            });
-            if (act) {
-                vstore_row<C>(a.dk + ti.row * a.ks, dka, a.scale);
-                vstore_row<C>(a.dv + ti.row * a.vs, dva, 1.0f);
-            }
+        };
+        if (v.masked) run(bool_c<true>{});
+        else run(bool_c<false>{});
+        if (act) {
+            const float sc = a.scale * ifs;
+            *reinterpret_cast<f4*>(a.dq + ti.row * a.qs + 4 * un.P) =
+                (f4){dq0.x * sc, dq0.y * sc, dq1.x * sc, dq1.y * sc};
         }
     }
     __syncthreads();
@@ -424,34 +418,131 @@ __global__ __launch_bounds__(512, 2) void wattn_bwd_sk_kernel(WAArgs a, int nq, 
     }
 }
 
+// pass B: lane = key row -> dk, dv (no LDS).  The x-row of queries is fetched in halves (12
+// SGPRs of q / dO / lse / delta per query).
+template <int NH, int WW>
+__global__ __launch_bounds__(1024) void wattn_bwdkv_sk_kernel(WAArgs a, int nq, int nunits, const float* delta) {
+    constexpr int NP = NH / 2;
+    constexpr int KC = WW ? WW : 1;
+    constexpr int HB = (KC % 2 == 0) ? KC / 2 : KC;   // queries fetched per batch
+    const WGeom& g = a.g;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wpb = blockDim.x >> 6;   // = nq * NP: one block walks one window per iteration
+    const f2 L2E = splat(kLog2e);
+    const float sl2 = a.scale * kLog2e;
+    const uint32_t qs4 = (uint32_t)a.qs * 4, os4 = (uint32_t)a.os * 4, ns4 = NH * 4;
+    for (int w = blockIdx.x; w < g.nwin; w += gridDim.x) {
+        const Unit un = {w, wave / NP, wave % NP};
+        const Win v = window_of(g, un.w);
+        const int t = un.qt * 64 + lane;
+        const bool act = t < g.N;
+        const TokenInfo ti = token_info(g, un.w, act ? t : g.N - 1);
+        const f4 k4 = vload4(a.k + ti.row * a.ks + 4 * un.P);
+        const f4 v4 = vload4(a.v + ti.row * a.vs + 4 * un.P);
+        const f2 kr0 = lo2(k4) * splat(sl2), kr1 = hi2(k4) * splat(sl2);
+        const f2 vr0 = lo2(v4), vr1 = hi2(v4);
+        const int cko = g.off - ti.code, rk = ti.rc;
+        const float* tabP = a.table + 2 * un.P;
+        const char* qP = reinterpret_cast<const char*>(a.q + 4 * un.P);
+        const char* gP = reinterpret_cast<const char*>(a.dout + 4 * un.P);
+        const char* lP = reinterpret_cast<const char*>(a.lse + 2 * un.P);
+        const char* dP = reinterpret_cast<const char*>(delta + 2 * un.P);
+        f2 dk0 = splat(0.f), dk1 = splat(0.f), dv0 = splat(0.f), dv1 = splat(0.f);
+        auto run = [&](auto masked_c) {
+            constexpr bool MASKED = decltype(masked_c)::value;
+            walk_window<WW>(g, v, [&](const int (&rows)[KC], int code0, const int (&rcs)[KC]) {
+#pragma unroll
+                for (int h0 = 0; h0 < KC; h0 += HB) {
+                    f4 qq[HB], gg[HB];
+                    f2 ll[HB], dd[HB], tb[HB];
+                    const float* tp = tabP + (code0 + h0 + cko) * NH;
+#pragma unroll
+                    for (int c = 0; c < HB; ++c) {
+                        const uint32_t r = (uint32_t)rows[h0 + c];
+                        qq[c] = sload4(qP, r * qs4);
+                        gg[c] = sload4(gP, r * os4);
+                        ll[c] = sload2(lP, r * ns4);
+                        dd[c] = sload2(dP, r * ns4);
+                        tb[c] = vload2(tp + c * NH);
+                    }
+#pragma unroll
+                    for (int c = 0; c < HB; ++c) {
+                        f2 base = pfma(tb[c], L2E, -ll[c]);
+                        if constexpr (MASKED) base += splat(rcs[h0 + c] != rk ? kMask2 : 0.f);
+                        f2 sc = pfma(lo2(qq[c]), kr0, base);
+                        sc = pfma(hi2(qq[c]), kr1, sc);
+                        const f2 pr = exp2_2(sc);
+                        const f2 tt = pfma(lo2(gg[c]), vr0, hi2(gg[c]) * vr1);
+                        const f2 dsv = pr * (tt - dd[c]);
+                        dv0 = pfma(pr, lo2(gg[c]), dv0);
+                        dv1 = pfma(pr, hi2(gg[c]), dv1);
+                        dk0 = pfma(dsv, lo2(qq[c]), dk0);
+                        dk1 = pfma(dsv, hi2(qq[c]), dk1);
+                    }
+                }
+            });
+        };
+        if (v.masked) run(bool_c<true>{});
+        else run(bool_c<false>{});
+        if (act) {
+            *reinterpret_cast<f4*>(a.dk + ti.row * a.ks + 4 * un.P) =
+                (f4){dk0.x * a.scale, dk0.y * a.scale, dk1.x * a.scale, dk1.y * a.scale};
+            *reinterpret_cast<f4*>(a.dv + ti.row * a.vs + 4 * un.P) = (f4){dv0.x, dv0.y, dv1.x, dv1.y};
+        }
+    }
+}
+
 }  // namespace sk
 
 // ------------------------------------------------------------------------------------
 // host side (called from wattn.hip for layout 1)
 // ------------------------------------------------------------------------------------
-static int sk_units(const WGeom& g, int& nq) {
+// block = the nq * NP units of one window; grid-stride over windows, sized to the resident capacity
+static int sk_units(const WGeom& g, int heads, int& nq) {
     nq = (g.N + 63) / 64;
-    return g.nwin * nq;
+    return g.nwin * nq * (heads / 2);
 }
 
-int wattn_sk_fwd(const WAArgs& a, int C, hipStream_t stream) {
+static int sk_block(const WGeom& g, int heads) { return 64 * ((g.N + 63) / 64) * (heads / 2); }
+
+static int sk_grid(const WGeom& g, int heads, int waves_per_cu) {
+    const int wpb = sk_block(g, heads) / 64;
+    int per_cu = waves_per_cu / wpb;
+    if (per_cu < 1) per_cu = 1;
+    return g.nwin < per_cu * kNumCU ? g.nwin : per_cu * kNumCU;
+}
+
+#define MMNI_SK_DISPATCH(KERN, NH_, ...)                                           \
+    (a.g.ww == 6 ? reinterpret_cast<void*>(&sk::KERN<NH_, 6>) : reinterpret_cast<void*>(&sk::KERN<NH_, 0>))
+
+// 32-bit byte offsets in the kernels: rows * stride * 4 must stay below 2^31 for every buffer
+static int sk_check_offsets(const WAArgs& a) {
+    const int64_t T = (int64_t)a.g.B * a.g.D * a.g.H * a.g.W;
+    int64_t smax = a.qs > a.ks ? a.qs : a.ks;
+    if (a.vs > smax) smax = a.vs;
+    if (a.os > smax) smax = a.os;
+    MMNI_ARG_CHECK(T * smax * 4 < (1ll << 31),
+                   "wattn (pair layout): %lld rows x stride %lld exceed the 2 GiB byte-offset range; split the "
+                   "batch or use layout 0", (long long)T, (long long)smax);
+    return 0;
+}
+
+int wattn_sk_fwd(const WAArgs& a0, int C, hipStream_t stream) {
+    WAArgs a = a0;
+    if (int rc = sk_check_offsets(a)) return rc;
     int nq;
-    const int units = sk_units(a.g, nq);
-    const int wpb = 8;
-    int grid = (units + wpb - 1) / wpb;
-    if (grid > 5 * kNumCU / 2) grid = 5 * kNumCU / 2;   // 5 waves per SIMD at <= 96 VGPRs
-    const bool w6 = a.g.ww == 6;
-    if (C == 12) {
-        if (w6) sk::wattn_fwd_sk_kernel<12, 3, 6><<<grid, 64 * wpb, 0, stream>>>(a, nq, units);
-        else sk::wattn_fwd_sk_kernel<12, 3, 0><<<grid, 64 * wpb, 0, stream>>>(a, nq, units);
-    } else if (C == 24) {
-        if (w6) sk::wattn_fwd_sk_kernel<24, 3, 6><<<grid, 64 * wpb, 0, stream>>>(a, nq, units);
-        else sk::wattn_fwd_sk_kernel<24, 3, 0><<<grid, 64 * wpb, 0, stream>>>(a, nq, units);
-    } else {
-        set_error("wattn (pair layout): C=%d unsupported (12 or 24)", C);
-        return -2;
-    }
-    return launch_status("wattn_fwd_sk");
+    const int heads = C / 2;
+    int units = sk_units(a.g, heads, nq);
+    void* kern = nullptr;
+    if (C == 12) kern = MMNI_SK_DISPATCH(wattn_fwd_sk_kernel, 6);
+    else if (C == 24) kern = MMNI_SK_DISPATCH(wattn_fwd_sk_kernel, 12);
+    else { set_error("wattn (pair layout): C=%d unsupported (12 or 24)", C); return -2; }
+    void* args[] = {&a, &nq, &units};
+    MMNI_ARG_CHECK(sk_block(a.g, heads) <= 1024, "wattn (pair layout): window of %d tokens too large", a.g.N);
+    hipError_t e = hipLaunchKernel(kern, dim3(sk_grid(a.g, heads, 32)), dim3(sk_block(a.g, heads)), args, 0, stream);
+    if (e != hipSuccess) { set_error("wattn_fwd_sk launch: %s", hipGetErrorString(e)); return (int)e; }
+    return 0;
 }
 
 size_t wattn_sk_workspace(const WGeom& g, int heads) {
@@ -460,33 +551,32 @@ size_t wattn_sk_workspace(const WGeom& g, int heads) {
 
 int wattn_sk_bwd(const WAArgs& a0, int C, int heads, void* workspace, hipStream_t stream) {
     WAArgs a = a0;
+    if (int rc = sk_check_offsets(a)) return rc;
     const WGeom& g = a.g;
     const int ntab = g.Tsz * heads;
     a.dtab_fix = reinterpret_cast<unsigned long long*>(workspace);
     a.maxbits = reinterpret_cast<unsigned int*>(a.dtab_fix + ntab);
-    float* delta = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + (size_t)ntab * 8 + 16);
+    const float* delta = reinterpret_cast<const float*>(reinterpret_cast<char*>(workspace) + (size_t)ntab * 8 + 16);
+    float* delta_w = const_cast<float*>(delta);
     hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8 + 16, stream);
     if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
     const int64_t T = (int64_t)g.nwin * g.N;
     int nq;
-    const int units = sk_units(g, nq);
-    const int wpb = 8;
-    int grid = (units + wpb - 1) / wpb;
-    if (grid > 2 * kNumCU) grid = 2 * kNumCU;
+    int units = sk_units(g, heads, nq);
     const size_t lds = (size_t)g.Tsz * (heads + 1) * 8;
     if (lds > 80 * 1024) {
         set_error("wattn_bwd (pair layout): table-gradient LDS %zu B exceeds 80 KiB", lds);
         return -2;
     }
-    void* kern = nullptr;
+    void *kq = nullptr, *kkv = nullptr;
     if (C == 12) {
-        sk::wattn_prep_sk_kernel<12><<<1024, 256, 0, stream>>>(a.o, a.dout, a.os, a.v, a.vs, T, delta, a.maxbits);
-        kern = a.g.ww == 6 ? reinterpret_cast<void*>(&sk::wattn_bwd_sk_kernel<12, 6>)
-                           : reinterpret_cast<void*>(&sk::wattn_bwd_sk_kernel<12, 0>);
+        sk::wattn_prep_sk_kernel<12><<<1024, 256, 0, stream>>>(a.o, a.dout, a.os, a.v, a.vs, T, delta_w, a.maxbits);
+        kq = MMNI_SK_DISPATCH(wattn_bwdq_sk_kernel, 6);
+        kkv = MMNI_SK_DISPATCH(wattn_bwdkv_sk_kernel, 6);
     } else if (C == 24) {
-        sk::wattn_prep_sk_kernel<24><<<1024, 256, 0, stream>>>(a.o, a.dout, a.os, a.v, a.vs, T, delta, a.maxbits);
-        kern = a.g.ww == 6 ? reinterpret_cast<void*>(&sk::wattn_bwd_sk_kernel<24, 6>)
-                           : reinterpret_cast<void*>(&sk::wattn_bwd_sk_kernel<24, 0>);
+        sk::wattn_prep_sk_kernel<24><<<1024, 256, 0, stream>>>(a.o, a.dout, a.os, a.v, a.vs, T, delta_w, a.maxbits);
+        kq = MMNI_SK_DISPATCH(wattn_bwdq_sk_kernel, 12);
+        kkv = MMNI_SK_DISPATCH(wattn_bwdkv_sk_kernel, 12);
     } else {
         set_error("wattn (pair layout): C=%d unsupported (12 or 24)", C);
         return -2;
@@ -494,14 +584,18 @@ int wattn_sk_bwd(const WAArgs& a0, int C, int heads, void* workspace, hipStream_
     int rc = launch_status("wattn_prep_sk");
     if (rc) return rc;
     if (lds > 64 * 1024) {
-        e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        e = hipFuncSetAttribute(kq, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         if (e != hipSuccess) { set_error("hipFuncSetAttribute: %s", hipGetErrorString(e)); return (int)e; }
     }
-    int nq_ = nq, units_ = units;
-    const float* delta_c = delta;
-    void* args[] = {&a, &nq_, &units_, &delta_c};
-    e = hipLaunchKernel(kern, dim3(grid), dim3(64 * wpb), args, lds, stream);
-    if (e != hipSuccess) { set_error("wattn_bwd_sk launch: %s", hipGetErrorString(e)); return (int)e; }
+    void* args[] = {&a, &nq, &units, &delta};
+    MMNI_ARG_CHECK(sk_block(g, heads) <= 1024, "wattn (pair layout): window of %d tokens too large", g.N);
+    const int per_cu_lds = (int)((160 * 1024) / lds);
+    const int wpb = sk_block(g, heads) / 64;
+    e = hipLaunchKernel(kq, dim3(sk_grid(g, heads, per_cu_lds * wpb < 32 ? per_cu_lds * wpb : 32)),
+                        dim3(sk_block(g, heads)), args, lds, stream);
+    if (e != hipSuccess) { set_error("wattn_bwdq_sk launch: %s", hipGetErrorString(e)); return (int)e; }
+    e = hipLaunchKernel(kkv, dim3(sk_grid(g, heads, 32)), dim3(sk_block(g, heads)), args, 0, stream);
+    if (e != hipSuccess) { set_error("wattn_bwdkv_sk launch: %s", hipGetErrorString(e)); return (int)e; }
     return 0;
 }
 
