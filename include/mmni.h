@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 2
+#define MMNI_ABI_VERSION 1
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -64,12 +64,6 @@ typedef struct mmni_wattn_desc {
     int64_t k_stride;
     int64_t v_stride;
     int64_t o_stride;           /* output rows (and dq/dk/dv rows use q/k/v strides)      */
-    int32_t layout;             /* 0: natural channels, element (h, c) at h*head_dim + c.
-                                   1: head pairs (kind 0, head_dim 2, even heads, C 12/24):
-                                      (h, c) at (h/2)*4 + c*2 + h%2 in q/k/v/out/dq/dk/dv rows,
-                                      and lse in base 2.  Scalar-key kernels (wattn_sk.hip);
-                                      callers permute their projection weights instead of
-                                      the activations.               */
 } mmni_wattn_desc;
 
 /* Forward.  table: (Tsz, heads) row-major with Tsz = (2wd-1)(2wh-1)(2ww-1), indexed by
@@ -79,8 +73,7 @@ typedef struct mmni_wattn_desc {
  * tau: kind 1 only, (heads) = exp(min(logit_scale, ln 100)) (swin_v2_module.py:154-156).
  * Shift mask: -100 between tokens of different shift regions (swinfusion_module.py:317-338),
  *   computed analytically from region ids, never materialised.
- * out: rows with o_stride; lse: (B*D*H*W, heads) softmax normaliser per row, natural log
- *   (layout 0) or base 2 (layout 1). */
+ * out: rows with o_stride; lse: (B*D*H*W, heads) natural-log softmax normaliser per row. */
 int mmni_wattn_fwd(const mmni_wattn_desc* d,
                    const float* q, const float* k, const float* v,
                    const float* table, const float* tau,

@@ -11,10 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MMNI_LIB selects another in-tree build of the same library (kernel experiments,
-# scripts/build_variant.sh); the default is the package's libmmni.so.
-LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 2
+LIB_PATH = os.path.join(_HERE, "libmmni.so")
+ABI_VERSION = 1
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -29,8 +27,7 @@ class WAttnDesc(ctypes.Structure):
                 ("wd", _c_i32), ("wh", _c_i32), ("ww", _c_i32),
                 ("sd", _c_i32), ("sh", _c_i32), ("sw", _c_i32),
                 ("kind", _c_i32), ("scale", _c_f),
-                ("q_stride", _c_i64), ("k_stride", _c_i64), ("v_stride", _c_i64), ("o_stride", _c_i64),
-                ("layout", _c_i32)]
+                ("q_stride", _c_i64), ("k_stride", _c_i64), ("v_stride", _c_i64), ("o_stride", _c_i64)]
 
 
 class MhaDesc(ctypes.Structure):

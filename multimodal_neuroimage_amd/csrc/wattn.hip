@@ -642,10 +642,6 @@ static int fill_args(const mmni_wattn_desc* d, WAArgs& a, int& HD) {
     MMNI_ARG_CHECK(d->q_stride >= d->C && d->k_stride >= d->C && d->v_stride >= d->C && d->o_stride >= d->C,
                    "wattn: token strides must be >= C");
     HD = d->C / d->heads;
-    MMNI_ARG_CHECK(d->layout == 0 || d->layout == 1, "wattn: layout must be 0 or 1");
-    MMNI_ARG_CHECK(d->layout == 0 || (d->kind == 0 && HD == 2 && d->heads % 2 == 0 && (d->C == 12 || d->C == 24)),
-                   "wattn: layout 1 (head pairs) needs kind 0, head_dim 2, even heads, C 12 or 24 "
-                   "(got kind %d, C %d, heads %d)", d->kind, d->C, d->heads);
     a.kind = d->kind;
     a.scale = d->scale;
     a.qs = d->q_stride; a.ks = d->k_stride; a.vs = d->v_stride; a.os = d->o_stride;
@@ -681,10 +677,6 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     MMNI_ARG_CHECK(row_aligned(q, d->q_stride, d->C) && row_aligned(k, d->k_stride, d->C) &&
                        row_aligned(v, d->v_stride, d->C) && row_aligned(out, d->o_stride, d->C),
                    "wattn_fwd: q/k/v/out must be 16-byte aligned with strides multiple of 4");
-    if (d->layout == 1) {
-        a.q = q; a.k = k; a.v = v; a.table = table; a.tau = table; a.out = out; a.lse = lse;
-        return wattn_sk_fwd(a, d->C, (hipStream_t)stream);
-    }
     void *kf, *kb;
     int maxt;
     bool packed = false;
@@ -706,7 +698,6 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
 extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
     WGeom g;
     if (make_geom(d, g)) return 0;
-    if (d->layout == 1) return wattn_sk_workspace(g, d->heads);
     return (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16;   // + the two absmax words
 }
 
@@ -727,17 +718,6 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                        row_aligned(dout, d->o_stride, d->C) && row_aligned(dq, d->q_stride, d->C) &&
                        row_aligned(dk, d->k_stride, d->C) && row_aligned(dv, d->v_stride, d->C),
                    "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
-    if (d->layout == 1) {
-        a.q = q; a.k = k; a.v = v; a.table = table; a.tau = table; a.lse = const_cast<float*>(lse);
-        a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtable;
-        rc = wattn_sk_bwd(a, d->C, d->heads, workspace, (hipStream_t)stream);
-        if (rc) return rc;
-        const int ntab = a.g.Tsz * d->heads;
-        const unsigned long long* fix = reinterpret_cast<const unsigned long long*>(workspace);
-        wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-            fix, reinterpret_cast<const unsigned int*>(fix + ntab), HD, dtable, ntab);
-        return launch_status("wattn_dtable_convert");
-    }
     void *kf, *kb;
     int maxt;
     bool packed = false;

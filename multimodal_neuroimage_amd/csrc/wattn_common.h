@@ -82,11 +82,6 @@ constexpr int kPkChunk = 6;                 // keys per online-softmax chunk (pa
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
 int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b);
 
-// Scalar-key kernels for the head-pair layout (wattn_sk.hip, layout 1, kind 0, head_dim 2).
-int wattn_sk_fwd(const WAArgs& a, int C, hipStream_t stream);
-int wattn_sk_bwd(const WAArgs& a, int C, int heads, void* workspace, hipStream_t stream);
-size_t wattn_sk_workspace(const WGeom& g, int heads);
-
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
 // backward on gfx950 (measured: 27.8 ms vs 4.8 ms without the table update at the C3 shape),

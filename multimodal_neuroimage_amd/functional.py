@@ -101,9 +101,8 @@ class WindowGeometry:
         return WindowGeometry(int(B), spatial, window, shift)
 
 
-def _wattn_desc(g, C, heads, kind, scale, qs, ks, vs, os_, layout=0):
+def _wattn_desc(g, C, heads, kind, scale, qs, ks, vs, os_):
     d = _lib.WAttnDesc()
-    d.layout = layout
     d.B = g.B
     d.D, d.H, d.W = g.spatial
     d.C = C
@@ -126,12 +125,11 @@ class _WindowAttention(torch.autograd.Function):
 
     q_src: (rows, Cq_total) with q in columns [0, C); kv_src: (rows, Ckv_total) with k in
     [k_off, k_off+C) and v in [v_off, v_off+C).  For self attention q_src is kv_src (packed
-    qkv, offsets 0/C/2C).  Returns (rows, C).  layout 1: every C-wide block in head-pair order
-    (pair_perm) -- the scalar-key kernels (wattn_sk.hip); lse is then base 2.
+    qkv, offsets 0/C/2C).  Returns (rows, C).
     """
 
     @staticmethod
-    def forward(ctx, q_src, kv_src, table, tau, geom, heads, kind, scale, k_off, v_off, packed, layout):
+    def forward(ctx, q_src, kv_src, table, tau, geom, heads, kind, scale, k_off, v_off, packed):
         C = q_src.shape[1] // 3 if packed else q_src.shape[1]
         require_device(q_src, kv_src, table, tau, what="window_attention")
         rows = q_src.shape[0]
@@ -144,7 +142,7 @@ class _WindowAttention(torch.autograd.Function):
         q = q_src
         k = kv_src[:, k_off:]
         v = kv_src[:, v_off:]
-        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C, layout)
+        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
         ev = KernelTimer.start()
         check(L.mmni_wattn_fwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau_c), ptr(out), ptr(lse),
@@ -152,13 +150,13 @@ class _WindowAttention(torch.autograd.Function):
         # SURVEY §8d counting: fwd 4*T*N*C FLOPs, 4*T*C*4 bytes (q, k, v read, o written)
         KernelTimer.stop(f"wattn_fwd_k{kind}_C{C}_N{geom.N}", ev, 4.0 * rows * geom.N * C, 16.0 * rows * C)
         ctx.save_for_backward(q_src, kv_src, table, tau_c, out, lse)
-        ctx.cfg = (geom, heads, kind, scale, k_off, v_off, packed, C, layout)
+        ctx.cfg = (geom, heads, kind, scale, k_off, v_off, packed, C)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         q_src, kv_src, table, tau, out, lse = ctx.saved_tensors
-        geom, heads, kind, scale, k_off, v_off, packed, C, layout = ctx.cfg
+        geom, heads, kind, scale, k_off, v_off, packed, C = ctx.cfg
         dout = dout.contiguous()
         if packed:
             dq_src = torch.empty_like(q_src)
@@ -172,7 +170,7 @@ class _WindowAttention(torch.autograd.Function):
         dtau = torch.zeros_like(tau) if tau is not None else None
         q, k, v = q_src, kv_src[:, k_off:], kv_src[:, v_off:]
         dq, dk, dv = dq_src, dkv_src[:, k_off:], dkv_src[:, v_off:]
-        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C, layout)
+        d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
         ws = torch.empty(L.mmni_wattn_bwd_workspace_bytes(d) // 8, device=q_src.device, dtype=torch.int64)
         ev = KernelTimer.start()
@@ -184,27 +182,11 @@ class _WindowAttention(torch.autograd.Function):
         KernelTimer.stop(f"wattn_bwd_k{kind}_C{C}_N{geom.N}", ev, 10.0 * rows * geom.N * C,
                          32.0 * rows * C + 4.0 * rows * heads)
         if packed:
-            return dq_src, None, dtable, dtau, None, None, None, None, None, None, None, None
-        return dq_src, dkv_src, dtable, dtau, None, None, None, None, None, None, None, None
+            return dq_src, None, dtable, dtau, None, None, None, None, None, None, None
+        return dq_src, dkv_src, dtable, dtau, None, None, None, None, None, None, None
 
 
-def pair_perm(C, heads):
-    """Index map natural -> head-pair channel order of one C-wide block (layout 1 of
-    mmni_wattn_desc): out[:, pair_perm] is the pair-ordered row; the map is an involution."""
-    hd = C // heads
-    assert hd == 2 and heads % 2 == 0, "head-pair layout needs head_dim 2 and an even head count"
-    perm = [0] * C
-    for h in range(heads):
-        for c in range(2):
-            perm[(h // 2) * 4 + c * 2 + (h % 2)] = h * 2 + c
-    return perm
-
-
-def pair_layout_ok(C, heads, kind=0):
-    return kind == 0 and heads > 0 and C % heads == 0 and C // heads == 2 and heads % 2 == 0 and C in (12, 24)
-
-
-def window_attention_self(qkv, table, geom, heads, *, kind=0, scale=None, tau=None, layout=0):
+def window_attention_self(qkv, table, geom, heads, *, kind=0, scale=None, tau=None):
     """Self window attention on packed qkv token rows (rows, 3C) -> (rows, C)."""
     C = qkv.shape[-1] // 3
     qkv2 = qkv.reshape(-1, 3 * C)
@@ -212,17 +194,17 @@ def window_attention_self(qkv, table, geom, heads, *, kind=0, scale=None, tau=No
         qkv2 = qkv2.contiguous()
     if scale is None:
         scale = (C // heads) ** -0.5
-    return _WindowAttention.apply(qkv2, qkv2, table, tau, geom, heads, kind, scale, C, 2 * C, True, layout)
+    return _WindowAttention.apply(qkv2, qkv2, table, tau, geom, heads, kind, scale, C, 2 * C, True)
 
 
-def window_attention_cross(q, kv, table, geom, heads, *, kind=0, scale=None, tau=None, layout=0):
+def window_attention_cross(q, kv, table, geom, heads, *, kind=0, scale=None, tau=None):
     """Cross window attention: q rows (rows, C) from x, kv rows (rows, 2C) from y."""
     C = q.shape[-1]
     q2 = q.reshape(-1, C).contiguous()
     kv2 = kv.reshape(-1, 2 * C).contiguous()
     if scale is None:
         scale = (C // heads) ** -0.5
-    return _WindowAttention.apply(q2, kv2, table, tau, geom, heads, kind, scale, 0, C, False, layout)
+    return _WindowAttention.apply(q2, kv2, table, tau, geom, heads, kind, scale, 0, C, False)
 
 
 def window_rows(geom, device):

@@ -1,16 +1,15 @@
 #!/bin/bash
-# SQ / SQC counters on the window-attention micro-benchmark (layout 1 by default), one pass per
-# counter group (8 SQ slots each).  usage: bash scripts/gpu_pmc_wattn.sh <tag> [layout]
+# SQ counters on the window-attention micro-benchmark, one pass per counter group (8 SQ slots
+# each).  usage: bash scripts/gpu_pmc_wattn.sh <tag>
 R="$GRAFT_REPO_ROOT"
 cd /tmp && export TMPDIR=/tmp
 out="$R/gpurun_out/pmc_wattn${1:+_$1}"
-lay=${2:-1}
 mkdir -p "$out"
 timeout -k 10 120 rocprofv3 -L > "$out/avail.txt" 2>&1 || true
 run() {  # name counters...
   local n=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "wattn" -f csv -d "$out/$n" -o w -- \
-      python3 "$R/scripts/bench_wattn.py" 2 $lay > "$out/$n.log" 2>&1
+      python3 "$R/scripts/bench_wattn.py" 2 > "$out/$n.log" 2>&1
   local rc=$?; echo "$n rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$out/$n.log"; exit $rc; }
 }
 run p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS

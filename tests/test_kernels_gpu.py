@@ -72,11 +72,8 @@ WATTN = [
 ]
 
 
-@pytest.mark.parametrize("layout", [0, 1])
 @pytest.mark.parametrize("kind,C,heads,B,spatial,window,shift,cross", WATTN)
-def test_window_attention_fwd_bwd_vs_oracle(device, kind, C, heads, B, spatial, window, shift, cross, layout):
-    if layout == 1 and not MF.pair_layout_ok(C, heads, kind):
-        pytest.skip("head-pair layout covers kind 0, head_dim 2, even heads, C 12/24")
+def test_window_attention_fwd_bwd_vs_oracle(device, kind, C, heads, B, spatial, window, shift, cross):
     gen = torch.Generator().manual_seed(hash((kind, C, B, spatial, window, shift, cross)) % (2 ** 31))
     geom = MF.WindowGeometry(B, spatial, window, shift)
     rows = geom.tokens
@@ -95,26 +92,22 @@ def test_window_attention_fwd_bwd_vs_oracle(device, kind, C, heads, B, spatial, 
     (ref * gout).sum().backward()
     # HIP kernel (fp32)
     f = lambda t: t.float().to(device).requires_grad_(True)  # noqa: E731
-    # layout 1: every C-wide block in head-pair channel order (an involution)
-    pm = MF.pair_perm(C, heads) if layout == 1 else list(range(C))
     tab_d = f(table)
     tau_d = f(tau) if tau is not None else None
     if cross:
-        qd = f(q[:, pm])
-        kvd = f(torch.cat([k[:, pm], v[:, pm]], dim=1))
-        out = MF.window_attention_cross(qd, kvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d, layout=layout)
+        qd = f(q)
+        kvd = f(torch.cat([k, v], dim=1))
+        out = MF.window_attention_cross(qd, kvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
     else:
-        qkvd = f(torch.cat([q[:, pm], k[:, pm], v[:, pm]], dim=1))
-        out = MF.window_attention_self(qkvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d, layout=layout)
-    (out * gout[:, pm].float().to(device)).sum().backward()
+        qkvd = f(torch.cat([q, k, v], dim=1))
+        out = MF.window_attention_self(qkvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
+    (out * gout.float().to(device)).sum().backward()
     torch.cuda.synchronize()
-    out = out[:, pm]
     assert rel_err(out, ref) < TOL
     if cross:
         dq, dk, dv = qd.grad, kvd.grad[:, :C], kvd.grad[:, C:]
     else:
         dq, dk, dv = qkvd.grad[:, :C], qkvd.grad[:, C:2 * C], qkvd.grad[:, 2 * C:]
-    dq, dk, dv = dq[:, pm], dk[:, pm], dv[:, pm]
     assert rel_err(dq, leaves[0].grad) < TOL
     assert rel_err(dk, leaves[1].grad) < TOL
     assert rel_err(dv, leaves[2].grad) < TOL
