@@ -194,6 +194,27 @@ int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const float* w, c
                       void* stream);
 int mmni_token_linear_supported(int K, int N, int epi, int K2);
 
+/* Fused token MLP (mlp.hip): y = fc2(GELU(fc1(x))) (+ residual) with the hidden activation kept
+ * in registers (Mlp / Mlp_fusion, swin_v2_module.py:16-32, swinfusion_module.py:14-30; nn.GELU
+ * exact erf, dropout inactive), on the f32 MFMA.  Covers C = 12, hidden H = 48
+ * (mmni_mlp_supported).  w1: fc1.weight (H, C), b1 (H) nullable, w2: fc2.weight (C, H), b2 (C)
+ * nullable.  x / residual / y / dy / dx are contiguous (rows, C): ldx = ldy = C.
+ * Backward recomputes the hidden activation: dx overwritten (row stride ldx), dw1 / db1 / dw2 /
+ * db2 overwritten (fixed-order reduction, deterministic); the residual's gradient is dy itself and
+ * stays with the caller. */
+typedef struct mmni_mlp_desc {
+    int64_t rows;
+    int32_t C, H;
+    int64_t ldx, ldy;
+} mmni_mlp_desc;
+int mmni_mlp_supported(int C, int H);
+int mmni_mlp_fwd(const mmni_mlp_desc* d, const float* x, const float* w1, const float* b1,
+                 const float* w2, const float* b2, const float* residual, float* y, void* stream);
+size_t mmni_mlp_bwd_workspace_bytes(const mmni_mlp_desc* d);
+int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float* w1, const float* b1,
+                 const float* w2, const float* dy, float* dx, float* dw1, float* db1, float* dw2,
+                 float* db2, void* workspace, void* stream);
+
 int mmni_version(void);
 const char* mmni_last_error(void);
 

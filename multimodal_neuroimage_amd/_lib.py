@@ -48,6 +48,10 @@ class TLinDesc(ctypes.Structure):
                 ("ldx", _c_i64), ("ldy", _c_i64), ("ldaux", _c_i64), ("w_sn", _c_i64), ("w_sk", _c_i64)]
 
 
+class MlpDesc(ctypes.Structure):
+    _fields_ = [("rows", _c_i64), ("C", _c_i32), ("H", _c_i32), ("ldx", _c_i64), ("ldy", _c_i64)]
+
+
 # symbol -> (restype, argtypes); every symbol include/mmni.h declares
 SIGNATURES = {
     "mmni_version": (_c_int, []),
@@ -70,6 +74,10 @@ SIGNATURES = {
     "mmni_linear_dw": (_c_int, [_c_i64, _c_int, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "mmni_token_linear": (_c_int, [ctypes.POINTER(TLinDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmni_token_linear_supported": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
+    "mmni_mlp_supported": (_c_int, [_c_int, _c_int]),
+    "mmni_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 8),
+    "mmni_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
+    "mmni_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 12),
 }
 
 _lib = None

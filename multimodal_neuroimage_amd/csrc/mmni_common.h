@@ -37,4 +37,8 @@ __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_lo
 // Number of resident 64-lane waves a launch should aim for: 256 CUs x occupancy.
 constexpr int kNumCU = 256;
 
+// out[j] = sum_b part[b][j] over a (nparts, ncols) slab in a fixed order (deterministic); columns
+// j >= split go to out2[j - split] (tokenops.hip).
+void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s);
+
 }  // namespace mmni

@@ -147,8 +147,7 @@ __global__ __launch_bounds__(1024) void column_sum_kernel(const float* __restric
     }
 }
 
-static void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2,
-                       hipStream_t s) {
+void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
     if (ncols <= 16)
         column_sum_kernel<16><<<(ncols + 15) / 16, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
     else if (ncols <= 32)

@@ -547,6 +547,57 @@ class _Mlp(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2, (dy if ctx.needs_input_grad[5] else None)
 
 
+def _mlp_desc(rows, C, H, ldx, ldy):
+    d = _lib.MlpDesc()
+    d.rows, d.C, d.H, d.ldx, d.ldy = rows, C, H, ldx, ldy
+    return d
+
+
+class _FusedMlp(torch.autograd.Function):
+    """fc2(GELU(fc1(x))) (+ residual) in one HIP kernel per direction (mlp.hip, f32 MFMA): the
+    hidden activation never reaches HBM; backward recomputes it from x."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual):
+        H, C = w1.shape
+        x2 = x.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+        r2 = residual.reshape(-1, C).contiguous() if residual is not None else None
+        d = _mlp_desc(rows, C, H, C, C)
+        ev = KernelTimer.start()
+        check(_lib.load().mmni_mlp_fwd(ctypes.byref(d), ptr(x2), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(r2), ptr(y),
+                                       stream_handle(x2.device)), "mmni_mlp_fwd")
+        # algorithmic: 4*rows*C*H FLOPs (two GEMMs); bytes: x, y (+ residual) rows
+        KernelTimer.stop(f"mlp_fwd_{C}x{H}", ev, 4.0 * rows * C * H, 4.0 * rows * C * (3 if r2 is not None else 2))
+        ctx.save_for_backward(x2, w1, b1, w2)
+        ctx.has_b = (b1 is not None, b2 is not None)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, b1, w2 = ctx.saved_tensors
+        H, C = w1.shape
+        dy2 = dy.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+        dw1 = torch.empty_like(w1)
+        dw2 = torch.empty_like(w2)
+        db1 = torch.empty(H, device=x2.device, dtype=torch.float32)
+        db2 = torch.empty(C, device=x2.device, dtype=torch.float32)
+        L = _lib.load()
+        d = _mlp_desc(rows, C, H, C, C)
+        ws = torch.empty(L.mmni_mlp_bwd_workspace_bytes(ctypes.byref(d)) // 4, device=x2.device, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(L.mmni_mlp_bwd(ctypes.byref(d), ptr(x2), ptr(w1), ptr(b1), ptr(w2), ptr(dy2), ptr(dx), ptr(dw1), ptr(db1),
+                             ptr(dw2), ptr(db2), ptr(ws), stream_handle(x2.device)), "mmni_mlp_bwd")
+        # algorithmic: recompute (2*rows*C*H) + dgrad (2 GEMMs) + wgrad (2 GEMMs) = 10*rows*C*H
+        KernelTimer.stop(f"mlp_bwd_{C}x{H}", ev, 10.0 * rows * C * H, 4.0 * rows * C * 3)
+        return (dx.view(ctx.xshape), dw1, db1 if ctx.has_b[0] else None, dw2, db2 if ctx.has_b[1] else None,
+                dy if ctx.needs_input_grad[5] else None)
+
+
 def mlp(x, fc1, fc2, act, drop, residual=None):
     """The reference Mlp forward `drop(fc2(drop(act(fc1(x)))))` (+ residual) with the fused HIP
     path when act is exact nn.GELU, the dropouts are inactive and the shapes are compiled; else
@@ -554,6 +605,9 @@ def mlp(x, fc1, fc2, act, drop, residual=None):
     require_device(x, what="mlp")
     H, C = fc1.weight.shape
     O = fc2.weight.shape[0]
+    if (isinstance(act, torch.nn.GELU) and act.approximate == "none" and (drop.p == 0.0 or not drop.training)
+            and O == C and _lib.load().mmni_mlp_supported(C, H) and x.shape[-1] == C):
+        return _FusedMlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, residual)
     fused = (isinstance(act, torch.nn.GELU) and act.approximate == "none"
              and (drop.p == 0.0 or not drop.training)
              and _tlin_ok(C, H, 1) and _tlin_ok(O, H, 2, C) and _tlin_ok(H, C) and _tlin_ok(H, O)

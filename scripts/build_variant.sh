@@ -9,7 +9,8 @@ mkdir -p "$(dirname "$out")" /tmp/mmni_var
 objs=()
 for f in "$R"/multimodal_neuroimage_amd/csrc/*.hip; do
   o=/tmp/mmni_var/$(basename "$f").$$.o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -w "$@" -c "$f" -o "$o" &
+  extra=""; [ "$(basename "$f")" = mlp.hip ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -w $extra "$@" -c "$f" -o "$o" &
   objs+=("$o")
 done
 wait

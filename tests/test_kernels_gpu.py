@@ -291,11 +291,13 @@ def test_token_linear_fwd_dx_vs_torch_fp64(device, K, N, with_res):
         assert rel_err(dev[3].grad, leaves[3].grad) < TOL
 
 
-@pytest.mark.parametrize("C,H", [(12, 48)])
-def test_fused_mlp_gelu_vs_torch_fp64(device, C, H):
-    """fc1 + exact GELU + fc2 with the GELU fused forward and backward (pre-activation
-    recomputed in the fc2 input-gradient kernel) vs the float64 torch MLP."""
-    rows = 50003
+@pytest.mark.parametrize("path", ["mfma", "tokenlinear"])
+@pytest.mark.parametrize("rows,with_res", [(50003, True), (16, False), (33, True)])
+def test_fused_mlp_gelu_vs_torch_fp64(device, path, rows, with_res):
+    """fc1 + exact GELU + fc2 vs the float64 torch MLP, through both HIP paths: the one-kernel MFMA
+    MLP (mlp.hip, hidden activation in registers, recomputed in backward) and the token-linear
+    path with the GELU fused into the fc1 / fc2-input-gradient epilogues."""
+    C, H = 12, 48
     gen = torch.Generator().manual_seed(C + H)
     x = torch.randn(rows, C, generator=gen, dtype=torch.float64)
     w1 = torch.randn(H, C, generator=gen, dtype=torch.float64) * 0.4
@@ -311,12 +313,35 @@ def test_fused_mlp_gelu_vs_torch_fp64(device, C, H):
         fc1.weight.copy_(w1.float()); fc1.bias.copy_(b1.float())
         fc2.weight.copy_(w2.float()); fc2.bias.copy_(b2.float())
     xd = x.float().to(device).requires_grad_(True)
-    rd = torch.zeros(rows, C, device=device, requires_grad=True)
-    out = MF.mlp(xd, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0), residual=rd)
+    rd = torch.randn(rows, C, device=device, requires_grad=True) if with_res else None
+    if path == "mfma":
+        out = MF.mlp(xd, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0), residual=rd)
+    else:
+        out = MF._Mlp.apply(xd, fc1.weight, fc1.bias, fc2.weight, fc2.bias, rd)
     (out * g.float().to(device)).sum().backward()
     torch.cuda.synchronize()
+    if with_res:
+        ref = ref + rd.detach().double().cpu()
+        assert rel_err(rd.grad, g) < TOL
     assert rel_err(out, ref) < TOL
-    assert rel_err(rd.grad, g) < TOL
     got = [xd.grad, fc1.weight.grad, fc1.bias.grad, fc2.weight.grad, fc2.bias.grad]
     for a, r in zip(got, leaves):
         assert rel_err(a, r.grad) < TOL
+
+
+def test_fused_mlp_weight_grad_is_deterministic(device):
+    """The MFMA MLP's weight gradients reduce per-wave partials in a fixed order: bitwise equal
+    across runs."""
+    C, H, rows = 12, 48, 200000
+    torch.manual_seed(3)
+    fc1, fc2 = torch.nn.Linear(C, H).to(device), torch.nn.Linear(H, C).to(device)
+    x = torch.randn(rows, C, device=device, requires_grad=True)
+    g = torch.randn(rows, C, device=device)
+    grads = []
+    for _ in range(2):
+        for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias):
+            p.grad = None
+        MF.mlp(x, fc1, fc2, torch.nn.GELU(), torch.nn.Dropout(0.0)).backward(g)
+        grads.append([p.grad.clone() for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
