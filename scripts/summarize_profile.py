@@ -38,6 +38,12 @@ def bench_key(name):
     m = re.search(r"mmni::linear_dw_kernel<(\d+), (\d+)>", name)
     if m:
         return f"linear_dw_tiles{m.group(1)}x{m.group(2)}"
+    m = re.search(r"mmni::mlpk::(mlp_fwd|mlp_bwd)_kernel", name)
+    if m:
+        return f"{m.group(1)}_12x48"
+    m = re.search(r"mmni::token_linear_kernel<(\d+), (\d+), (\d), \d+>", name)
+    if m:
+        return f"token_linear_e{m.group(3)}_{m.group(1)}x{m.group(2)}"
     m = re.search(r"mmni::(wattn_absmax|wattn_dtable_convert|column_sum)_kernel", name)
     if m:
         return m.group(1)
