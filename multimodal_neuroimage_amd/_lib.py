@@ -11,7 +11,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmmni.so")
+# MMNI_LIB selects another in-tree build of the same library (kernel experiments,
+# scripts/build_variant.sh); the default is the package's libmmni.so.
+LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
 ABI_VERSION = 1
 
 _c_int = ctypes.c_int

@@ -77,7 +77,10 @@ struct WAArgs {
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
 constexpr float kNormEps = 1e-12f;          // F.normalize eps (swin_v2_module.py:153)
 constexpr int CH = 4;                       // keys per online-softmax chunk (generic kernels)
-constexpr int kPkChunk = 6;                 // keys per online-softmax chunk (packed kernels)
+#ifndef MMNI_PK_CHUNK
+#define MMNI_PK_CHUNK 6
+#endif
+constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
 int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b);
