@@ -215,6 +215,31 @@ int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float* w1, const 
                  const float* w2, const float* dy, float* dx, float* dw1, float* db1, float* dw2,
                  float* db2, void* workspace, void* stream);
 
+/* Fused token ops around the window attention of a SwinFusion block (blockops.hip, C = 12, f32
+ * MFMA), replacing norm1 + attn.qkv / attn.q / attn.kv and their backward with the block's
+ * residual gradient (swinfusion_module.py:346,121,202-205,377), and the backward of attn.proj
+ * (swinfusion_module.py:143).  Token rows contiguous and 16-byte aligned.
+ *   ln_linear_fwd   y (rows, N) = LN(x) W^T + b, LN over C with gamma/beta/eps (nn.LayerNorm);
+ *                   mean / rstd (rows) saved for the backward (the LN output is never stored).
+ *   ln_linear_bwd   dx = LN_bwd(dy W) + dres (dres nullable), dw (N, C), db (N, nullable),
+ *                   dgamma, dbeta (C): LN(x) recomputed from x, mean, rstd.  N = 12, 24, 36.
+ *   linear_bwd      dx = dy W, dw = dy^T x, db = colsum dy for a C -> C Linear (N = C).
+ * Gradients are overwritten; reductions run in a fixed order (deterministic). */
+typedef struct mmni_tok_desc {
+    int64_t rows;
+    int32_t C, N;
+    float eps;
+} mmni_tok_desc;
+int mmni_ln_linear_fwd(const mmni_tok_desc* d, const float* x, const float* gamma, const float* beta,
+                       const float* w, const float* b, float* y, float* mean, float* rstd, void* stream);
+size_t mmni_tok_bwd_workspace_bytes(const mmni_tok_desc* d);
+int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                       const float* rstd, const float* gamma, const float* beta, const float* w,
+                       const float* dres, float* dx, float* dw, float* db, float* dgamma,
+                       float* dbeta, void* workspace, void* stream);
+int mmni_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* w,
+                    float* dx, float* dw, float* db, void* workspace, void* stream);
+
 int mmni_version(void);
 const char* mmni_last_error(void);
 

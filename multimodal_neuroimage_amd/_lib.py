@@ -54,6 +54,10 @@ class MlpDesc(ctypes.Structure):
     _fields_ = [("rows", _c_i64), ("C", _c_i32), ("H", _c_i32), ("ldx", _c_i64), ("ldy", _c_i64)]
 
 
+class TokDesc(ctypes.Structure):
+    _fields_ = [("rows", _c_i64), ("C", _c_i32), ("N", _c_i32), ("eps", _c_f)]
+
+
 # symbol -> (restype, argtypes); every symbol include/mmni.h declares
 SIGNATURES = {
     "mmni_version": (_c_int, []),
@@ -80,6 +84,10 @@ SIGNATURES = {
     "mmni_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 8),
     "mmni_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
     "mmni_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 12),
+    "mmni_ln_linear_fwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 9),
+    "mmni_tok_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(TokDesc)]),
+    "mmni_ln_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 15),
+    "mmni_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 8),
 }
 
 _lib = None

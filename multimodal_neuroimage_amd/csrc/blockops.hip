@@ -1,0 +1,324 @@
+// Fused token ops around the window attention of a SwinFusion block,
+// C = 12 channels, on the f32 MFMA (tile maps: tokentile.h).
+//
+// Replaces, per SwinTransformerBlock_fusion (modules/swinfusion_module.py:340-380):
+//   norm1 + attn.qkv  (swinfusion_module.py:346, 121)   -> ln_linear_fwd   x -> qkv, (mean, rstd)
+//   backward of both + the residual gradient            -> ln_linear_bwd   dqkv, x, dres -> dx, dW, db, dgamma, dbeta
+//   backward of attn.proj (swinfusion_module.py:143)    -> linear_bwd      dy, o -> do, dW, db
+// The LayerNorm output is never stored: the backward recomputes it from x and the saved
+// (mean, rstd), so the qkv weight gradient, the qkv input gradient, the LayerNorm backward and
+// the residual add that autograd would issue separately are one pass over the token rows.
+// Weight / affine gradients are per-wave partials reduced in a fixed order (column_sum):
+// deterministic.
+#include "tokentile.h"
+
+namespace mmni {
+namespace blk {
+
+using namespace tt;
+
+struct TokArgs {
+    int64_t rows;
+    float eps;
+    const float* x;      // (rows, C)
+    const float* gamma;  // (C)
+    const float* beta;   // (C)
+    const float* w;      // (N, C) nn.Linear weight
+    const float* b;      // (N) or null
+    float* y;            // fwd: (rows, N)
+    float* mean;         // (rows)
+    float* rstd;         // (rows)
+    const float* dy;     // bwd: (rows, N)
+    const float* dres;   // bwd: (rows, C) residual gradient added to dx, or null
+    float* dx;           // bwd: (rows, C)
+    float* partA;        // [waves][N*C + N]  dW | db
+    float* partB;        // [waves][2C]       dgamma | dbeta
+};
+
+// ------------------------------------------------------------------------------------
+// y = LN(x) W^T + b, per 16-token tile: LN on the feature-major operand, NT MFMA output tiles
+// ------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
+    constexpr int NT = (N + 15) / 16;
+    const int lane = threadIdx.x & 63;
+    const Tile tl{a.rows, lane & 15, lane >> 4};
+    const int t = tl.t, g = tl.g;
+    const int64_t wave = __builtin_amdgcn_readfirstlane(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    float wa[NT][CS], gm[CS], bt[CS];
+    f4 bc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int n = nt * 16 + t;
+#pragma unroll
+        for (int s = 0; s < CS; ++s) wa[nt][s] = n < N ? a.w[n * C + 4 * s + g] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int nr = nt * 16 + 4 * g + i;
+            bc[nt][i] = (a.b && nr < N) ? a.b[nr] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < CS; ++s) { gm[s] = a.gamma[4 * s + g]; bt[s] = a.beta[4 * s + g]; }
+    const int64_t tiles = (a.rows + 15) / 16;
+    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
+        const int64_t t0 = tile * 16;
+        float v[CS];
+        tl.load_fm<CS, C>(a.x, t0, v);
+        float mean, rstd;
+        ln_stats(v, a.eps, mean, rstd);
+        float xn[CS];
+#pragma unroll
+        for (int s = 0; s < CS; ++s) xn[s] = fmaf((v[s] - mean) * rstd, gm[s], bt[s]);
+        const bool ok = tl.token_ok(t0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            f4 acc = bc[nt];
+#pragma unroll
+            for (int s = 0; s < CS; ++s) acc = mfma(wa[nt][s], xn[s], acc);
+            if (ok && nt * 16 + 4 * g < N) *reinterpret_cast<f4*>(a.y + (t0 + t) * N + nt * 16 + 4 * g) = acc;
+        }
+        if (ok && g == 0) {
+            a.mean[t0 + t] = mean;
+            a.rstd[t0 + t] = rstd;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// dx = LN_bwd(dy W) + dres;  dW = dy^T LN(x),  db = colsum dy,  dgamma, dbeta
+// ------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
+    constexpr int NT = (N + 15) / 16;
+    constexpr int NS = N / 4;   // k-steps over the N gradient columns
+    const int lane = threadIdx.x & 63;
+    const Tile tl{a.rows, lane & 15, lane >> 4};
+    const int t = tl.t, g = tl.g;
+    const int64_t wave = __builtin_amdgcn_readfirstlane(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    float wt[NS];                 // W^T[c = t][n = 4 s + g]
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wt[s] = t < C ? a.w[(4 * s + g) * C + t] : 0.f;
+    f4 gm4, bt4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        gm4[i] = g < 3 ? a.gamma[4 * g + i] : 0.f;
+        bt4[i] = g < 3 ? a.beta[4 * g + i] : 0.f;
+    }
+    const float gmt = t < C ? a.gamma[t] : 0.f, btt = t < C ? a.beta[t] : 0.f;
+    f4 dw[NT], dg = zero4(), dbt = zero4();
+    float db[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) { dw[nt] = zero4(); db[nt] = 0.f; }
+
+    const int64_t tiles = (a.rows + 15) / 16;
+    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
+        const int64_t t0 = tile * 16;
+        // dxn^T = W^T dy^T: accumulator chunk = dL/dLN(x) of channels 4 g + i of token t0 + t
+        float dyb[NS];
+        tl.load_fm<NS, N>(a.dy, t0, dyb);
+        f4 dxn = zero4();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) dxn = mfma(wt[s], dyb[s], dxn);
+        // LayerNorm backward on the chunk (+ residual gradient)
+        const bool ok = tl.chunk_ok(t0);
+        const bool tok = tl.token_ok(t0);
+        const float m = tok ? a.mean[t0 + t] : 0.f, rs = tok ? a.rstd[t0 + t] : 0.f;
+        const f4 xc = ok ? *reinterpret_cast<const f4*>(a.x + (t0 + t) * C + 4 * g) : zero4();
+        const f4 xh = ok ? (xc - m) * rs : zero4();
+        f4 dx = ln_bwd_chunk(dxn, xh, gm4, rs);
+        if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
+        if (ok) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
+        dg += dxn * xh;
+        dbt += dxn;
+        // dW = dy^T xn over the tile's tokens (token-major operands; xn recomputed)
+        float xa[4], mt[4], rt[4], xnt[4];
+        tl.load_tm<C>(a.x, t0, 0, C, xa);
+        tl.load_tm_scalar(a.mean, t0, mt);
+        tl.load_tm_scalar(a.rstd, t0, rt);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xnt[s] = t < C ? fmaf((xa[s] - mt[s]) * rt[s], gmt, btt) : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            float dya[4];
+            tl.load_tm<N>(a.dy, t0, nt * 16, N - nt * 16, dya);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                dw[nt] = mfma(dya[s], xnt[s], dw[nt]);
+                db[nt] += dya[s];
+            }
+        }
+    }
+    // per-wave partials: A = [dW (N x C) | db (N)], B = [dgamma (C) | dbeta (C)]
+    float* pa = a.partA + wave * (N * C + N);
+    float* pb = a.partB + wave * (2 * C);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = nt * 16 + 4 * g + i;
+            if (n < N && t < C) pa[n * C + t] = dw[nt][i];
+        }
+        const float v = sum_groups(db[nt]);
+        if (g == 0 && nt * 16 + t < N) pa[N * C + nt * 16 + t] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float a1 = sum_tokens(dg[i]), a2 = sum_tokens(dbt[i]);
+        if (t == 0 && g < 3) {
+            pb[4 * g + i] = a1;
+            pb[C + 4 * g + i] = a2;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// dx = dy W;  dW = dy^T x;  db = colsum dy   (a C -> C Linear: the attention proj)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void linear_bwd_kernel(TokArgs a) {
+    const int lane = threadIdx.x & 63;
+    const Tile tl{a.rows, lane & 15, lane >> 4};
+    const int t = tl.t, g = tl.g;
+    const int64_t wave = __builtin_amdgcn_readfirstlane(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    float wt[CS];
+#pragma unroll
+    for (int s = 0; s < CS; ++s) wt[s] = t < C ? a.w[(4 * s + g) * C + t] : 0.f;   // W^T[c = t][o = 4 s + g]
+    f4 dw = zero4();
+    float db = 0.f;
+    const int64_t tiles = (a.rows + 15) / 16;
+    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
+        const int64_t t0 = tile * 16;
+        float dyb[CS];
+        tl.load_fm<CS, C>(a.dy, t0, dyb);
+        f4 dx = zero4();
+#pragma unroll
+        for (int s = 0; s < CS; ++s) dx = mfma(wt[s], dyb[s], dx);
+        if (tl.chunk_ok(t0)) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
+        float dya[4], xa[4];
+        tl.load_tm<C>(a.dy, t0, 0, C, dya);
+        tl.load_tm<C>(a.x, t0, 0, C, xa);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            dw = mfma(dya[s], xa[s], dw);
+            db += dya[s];
+        }
+    }
+    float* pa = a.partA + wave * (C * C + C);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int o = 4 * g + i;
+        if (o < C && t < C) pa[o * C + t] = dw[i];
+    }
+    db = sum_groups(db);
+    if (g == 0 && t < C) pa[C * C + t] = db;
+}
+
+}  // namespace blk
+
+namespace {
+template <typename K>
+int waves_of(K kern) {
+    static_assert(sizeof(K) > 0, "");
+    return tt::resident_blocks(reinterpret_cast<const void*>(kern), 256, 0) * 4;
+}
+}  // namespace
+
+}  // namespace mmni
+
+using namespace mmni;
+
+static int tok_check(const mmni_tok_desc* d, bool ln) {
+    MMNI_ARG_CHECK(d != nullptr && d->rows > 0, "token op: empty descriptor");
+    MMNI_ARG_CHECK(d->C == 12, "token op: fused kernels cover C = 12 (got %d)", d->C);
+    MMNI_ARG_CHECK(ln ? (d->N == 12 || d->N == 24 || d->N == 36) : d->N == 12,
+                   "token op: unsupported N = %d", d->N);
+    return 0;
+}
+
+static bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+extern "C" int mmni_ln_linear_fwd(const mmni_tok_desc* d, const float* x, const float* gamma, const float* beta,
+                                  const float* w, const float* b, float* y, float* mean, float* rstd, void* stream) {
+    int rc = tok_check(d, true);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(x && gamma && beta && w && y && mean && rstd, "ln_linear_fwd: null pointer");
+    MMNI_ARG_CHECK(al16(x) && al16(y), "ln_linear_fwd: x / y must be 16-byte aligned");
+    blk::TokArgs a{};
+    a.rows = d->rows; a.eps = d->eps; a.x = x; a.gamma = gamma; a.beta = beta; a.w = w; a.b = b;
+    a.y = y; a.mean = mean; a.rstd = rstd;
+    const int64_t tiles = (d->rows + 15) / 16;
+    hipStream_t s = (hipStream_t)stream;
+#define MMNI_LLF(NN)                                                                                  \
+    if (d->N == NN) {                                                                                 \
+        static const int waves = waves_of(&blk::ln_linear_fwd_kernel<NN>);                          \
+        const int64_t grid = (tiles + 3) / 4 < waves / 4 ? (tiles + 3) / 4 : waves / 4;             \
+        blk::ln_linear_fwd_kernel<NN><<<(int)grid, 256, 0, s>>>(a);                                  \
+    }
+    MMNI_LLF(12) MMNI_LLF(24) MMNI_LLF(36)
+#undef MMNI_LLF
+    return launch_status("ln_linear_fwd");
+}
+
+extern "C" size_t mmni_tok_bwd_workspace_bytes(const mmni_tok_desc* d) {
+    if (!d) return 0;
+    // the widest grid any of the backward kernels uses: resident blocks of 4 waves, at most 8 per CU
+    const size_t waves = (size_t)kNumCU * 8 * 4;
+    return waves * ((size_t)d->N * d->C + d->N + 2 * d->C) * sizeof(float);
+}
+
+extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                                  const float* rstd, const float* gamma, const float* beta, const float* w,
+                                  const float* dres, float* dx, float* dw, float* db, float* dgamma, float* dbeta,
+                                  void* workspace, void* stream) {
+    int rc = tok_check(d, true);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(dy && x && mean && rstd && gamma && beta && w && dx && dw && dgamma && dbeta && workspace,
+                   "ln_linear_bwd: null pointer");
+    MMNI_ARG_CHECK(al16(x) && al16(dx) && (!dres || al16(dres)), "ln_linear_bwd: rows must be 16-byte aligned");
+    const int N = d->N, C = d->C;
+    blk::TokArgs a{};
+    a.rows = d->rows; a.x = x; a.gamma = gamma; a.beta = beta; a.w = w; a.mean = const_cast<float*>(mean);
+    a.rstd = const_cast<float*>(rstd); a.dy = dy; a.dres = dres; a.dx = dx;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t tiles = (d->rows + 15) / 16;
+    int waves = 0;
+#define MMNI_LLB(NN)                                                                                  \
+    if (N == NN) {                                                                                    \
+        static const int wv = waves_of(&blk::ln_linear_bwd_kernel<NN>);                             \
+        waves = wv < kNumCU * 8 * 4 ? wv : kNumCU * 8 * 4;                                           \
+        a.partA = reinterpret_cast<float*>(workspace);                                              \
+        a.partB = a.partA + (size_t)waves * (N * C + N);                                            \
+        blk::ln_linear_bwd_kernel<NN><<<waves / 4, 256, 0, s>>>(a);                                  \
+    }
+    MMNI_LLB(12) MMNI_LLB(24) MMNI_LLB(36)
+#undef MMNI_LLB
+    (void)tiles;
+    rc = launch_status("ln_linear_bwd");
+    if (rc) return rc;
+    column_sum(a.partA, waves, N * C + N, dw, N * C, db, s);
+    column_sum(a.partB, waves, 2 * C, dgamma, C, dbeta, s);
+    return launch_status("ln_linear_bwd_colsum");
+}
+
+extern "C" int mmni_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* w, float* dx,
+                               float* dw, float* db, void* workspace, void* stream) {
+    int rc = tok_check(d, false);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(dy && x && w && dx && dw && workspace, "linear_bwd: null pointer");
+    MMNI_ARG_CHECK(al16(dx), "linear_bwd: dx must be 16-byte aligned");
+    const int C = d->C;
+    blk::TokArgs a{};
+    a.rows = d->rows; a.x = x; a.w = w; a.dy = dy; a.dx = dx;
+    static const int wv = waves_of(&blk::linear_bwd_kernel);
+    const int waves = wv < kNumCU * 8 * 4 ? wv : kNumCU * 8 * 4;
+    a.partA = reinterpret_cast<float*>(workspace);
+    hipStream_t s = (hipStream_t)stream;
+    blk::linear_bwd_kernel<<<waves / 4, 256, 0, s>>>(a);
+    rc = launch_status("linear_bwd");
+    if (rc) return rc;
+    column_sum(a.partA, waves, C * C + C, dw, C * C, db, s);
+    return launch_status("linear_bwd_colsum");
+}

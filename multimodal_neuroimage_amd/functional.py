@@ -509,6 +509,10 @@ class _TokenLinear(torch.autograd.Function):
         N, K = weight.shape
         dy2 = _rows2d(dy, N)
         dx = None
+        if (N == K == TOK_C and ctx.needs_input_grad[0] and x2.is_contiguous() and dy2.is_contiguous()
+                and x2.data_ptr() % 16 == 0):
+            dx, dw, db = _linear_bwd_fused(x2, dy2, weight, ctx.has_bias)
+            return dx.view(ctx.xshape), dw, db, (dy if ctx.needs_input_grad[3] else None)
         if ctx.needs_input_grad[0]:
             dx = _tlin(dy2, weight, None, N, K, transposed=True) if _tlin_ok(N, K) else dy2 @ weight
             dx = dx.view(ctx.xshape)
@@ -616,6 +620,103 @@ def mlp(x, fc1, fc2, act, drop, residual=None):
         y = drop(linear(drop(act(linear(x, fc1))), fc2))
         return y if residual is None else residual + y
     return _Mlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, residual)
+
+
+# ----------------------------------------------------------------------------------------
+# fused LayerNorm -> Linear (norm1 + attn.qkv / q / kv of a SwinFusion block, blockops.hip)
+# ----------------------------------------------------------------------------------------
+TOK_C = 12
+TOK_LN_N = (12, 24, 36)
+
+
+def _tok_desc(rows, C, N, eps=0.0):
+    d = _lib.TokDesc()
+    d.rows, d.C, d.N, d.eps = rows, C, N, eps
+    return d
+
+
+class _LnLinear(torch.autograd.Function):
+    """y = LN(x) W^T + b in one pass; the LayerNorm output never reaches HBM (the backward
+    recomputes it from x and the saved row statistics).  With passthrough=True the Function also
+    returns x itself (a view) to be used as the block's residual: its gradient arrives here and is
+    added inside the fused backward instead of by a separate autograd add."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w, b, eps, passthrough):
+        N, C = w.shape
+        x2 = x.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty(rows, N, device=x2.device, dtype=torch.float32)
+        mean = torch.empty(rows, device=x2.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x2.device, dtype=torch.float32)
+        d = _tok_desc(rows, C, N, eps)
+        ev = KernelTimer.start()
+        check(_lib.load().mmni_ln_linear_fwd(ctypes.byref(d), ptr(x2), ptr(gamma), ptr(beta), ptr(w), ptr(b), ptr(y),
+                                             ptr(mean), ptr(rstd), stream_handle(x2.device)), "mmni_ln_linear_fwd")
+        # algorithmic: LN (~8 flops/elt) + 2*rows*C*N; bytes: x in, y + mean/rstd out
+        KernelTimer.stop(f"ln_linear_fwd_{C}x{N}", ev, 2.0 * rows * C * N + 8.0 * rows * C,
+                         4.0 * rows * (C + N + 2))
+        ctx.save_for_backward(x2, gamma, beta, w, mean, rstd)
+        ctx.has_b = b is not None
+        ctx.xshape = x.shape
+        y = y.view(*x.shape[:-1], N)
+        return (y, x.view(x.shape)) if passthrough else y
+
+    @staticmethod
+    def backward(ctx, dy, dres=None):
+        x2, gamma, beta, w, mean, rstd = ctx.saved_tensors
+        N, C = w.shape
+        rows = x2.shape[0]
+        dy2 = dy.reshape(-1, N).contiguous()
+        dr2 = dres.reshape(-1, C).contiguous() if dres is not None else None
+        dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+        dw = torch.empty_like(w)
+        db = torch.empty(N, device=x2.device, dtype=torch.float32) if ctx.has_b else None
+        dgamma = torch.empty(C, device=x2.device, dtype=torch.float32)
+        dbeta = torch.empty(C, device=x2.device, dtype=torch.float32)
+        L = _lib.load()
+        d = _tok_desc(rows, C, N)
+        ws = torch.empty(L.mmni_tok_bwd_workspace_bytes(ctypes.byref(d)) // 4, device=x2.device, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(L.mmni_ln_linear_bwd(ctypes.byref(d), ptr(dy2), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
+                                   ptr(w), ptr(dr2), ptr(dx), ptr(dw), ptr(db), ptr(dgamma), ptr(dbeta), ptr(ws),
+                                   stream_handle(x2.device)), "mmni_ln_linear_bwd")
+        KernelTimer.stop(f"ln_linear_bwd_{C}x{N}", ev, 4.0 * rows * C * N + 16.0 * rows * C,
+                         4.0 * rows * (N + 2 * C + 2 + (C if dr2 is not None else 0)))
+        return dx.view(ctx.xshape), dgamma, dbeta, dw, db, None, None
+
+
+def ln_linear_ok(x, norm, lin):
+    return (x.shape[-1] == TOK_C and isinstance(norm, torch.nn.LayerNorm) and norm.elementwise_affine
+            and norm.bias is not None and lin.weight.shape[1] == TOK_C and lin.weight.shape[0] in TOK_LN_N)
+
+
+def ln_linear(x, norm, lin, passthrough=False):
+    """lin(norm(x)) fused (x (..., 12), lin 12 -> 12/24/36); other shapes run LayerNorm and Linear
+    as separate HIP kernels.  passthrough=True also returns x for use as the residual (see
+    _LnLinear)."""
+    require_device(x, what="ln_linear")
+    if ln_linear_ok(x, norm, lin):
+        return _LnLinear.apply(x, norm.weight, norm.bias, lin.weight, lin.bias, float(norm.eps), passthrough)
+    y = linear(layer_norm(x, norm), lin)
+    return (y, x) if passthrough else y
+
+
+def _linear_bwd_fused(x2, dy2, weight, with_bias):
+    """dx, dW, db of a 12 -> 12 token Linear in one pass over (dy, x) (blockops.hip)."""
+    rows = x2.shape[0]
+    C = TOK_C
+    dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+    dw = torch.empty_like(weight)
+    db = torch.empty(C, device=x2.device, dtype=torch.float32) if with_bias else None
+    L = _lib.load()
+    d = _tok_desc(rows, C, C)
+    ws = torch.empty(L.mmni_tok_bwd_workspace_bytes(ctypes.byref(d)) // 4, device=x2.device, dtype=torch.float32)
+    ev = KernelTimer.start()
+    check(L.mmni_linear_bwd(ctypes.byref(d), ptr(dy2), ptr(x2), ptr(weight), ptr(dx), ptr(dw), ptr(db), ptr(ws),
+                            stream_handle(x2.device)), "mmni_linear_bwd")
+    KernelTimer.stop(f"linear_bwd_{C}x{C}", ev, 4.0 * rows * C * C, 4.0 * rows * C * 3)
+    return dx, dw, db
 
 
 def linear(x, lin_or_weight, bias=None, residual=None):

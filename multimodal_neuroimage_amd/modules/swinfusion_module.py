@@ -5,8 +5,8 @@ forward signatures and state_dict keys.  Inside, the shifted-windo
 every block is ONE HIP launch (libmmni.so: mmni_wattn_fwd/bwd) that reads the qkv projection
 straight from the un-partitioned channels-last token tensor: the roll, window_partition, mask
 rebuild + H2D copy, bias gather, softmax, AV, window_reverse and reverse roll of the reference
-(swinfusion_module.py:350-373, 114-145) collapse into it.  Projections, LayerNorm and the MLP
-stay on torch/hipBLASLt.  Every block also accepts 3D token grids (x_size = (D, H, W)), the
+(swinfusion_module.py:350-373, 114-145) collapse into it.  At C = 12 norm1 is fused into the
+qkv / q / kv projections (blockops.hip) and fc1 + GELU + fc2 is one kernel (mlp.hip).  Every block also accepts 3D token grids (x_size = (D, H, W)), the
 build's 3D lift; 2D inputs are the D = 1 special case.
 """
 import math
@@ -16,7 +16,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp
+from ..functional import (window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp, ln_linear,
+                          ln_linear_ok)
 from ._common import (DropPath, inactive, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -92,8 +93,11 @@ class WindowAttention_fusion(nn.Module):
 
     def forward_tokens(self, x, geom, residual=None):
         """Fused path: x (rows, C) un-partitioned token rows of geometry `geom` -> (rows, C)."""
+        return self.attend(linear(x, self.qkv), geom, residual)
+
+    def attend(self, qkv, geom, residual=None):
+        """Attention + proj (+ residual) from the projected (rows, 3C) qkv."""
         _no_attn_dropout(self)
-        qkv = linear(x, self.qkv)
         o = window_attention_self(qkv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                   scale=self.scale)
         if residual is not None and inactive(self.proj_drop):
@@ -141,9 +145,11 @@ class Cross_WindowAttention(nn.Module):
         self.softmax = nn.Softmax(dim=-1)
 
     def forward_tokens(self, x, y, geom, residual=None):
+        return self.attend(linear(x, self.q), linear(y, self.kv), geom, residual)
+
+    def attend(self, q, kv, geom, residual=None):
+        """Cross attention + proj (+ residual) from the projected q (rows, C) and kv (rows, 2C)."""
         _no_attn_dropout(self)
-        q = linear(x, self.q)
-        kv = linear(y, self.kv)
         o = window_attention_cross(q, kv, self.relative_position_bias_table, geom, self.num_heads, kind=0,
                                    scale=self.scale)
         if residual is not None and inactive(self.proj_drop):
@@ -194,6 +200,11 @@ class SwinTransformerBlock_fusion(nn.Module):
     def forward(self, x, x_size):
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
+        if inactive(self.drop_path) and ln_linear_ok(x, self.norm1, self.attn.qkv):
+            # norm1 + qkv in one kernel; the residual's gradient joins inside its backward
+            qkv, xr = ln_linear(x, self.norm1, self.attn.qkv, passthrough=True)
+            x = self.attn.attend(qkv.reshape(B * L, 3 * C), geom, residual=xr.reshape(B * L, C)).view(B, L, C)
+            return self.mlp(layer_norm(x, self.norm2), residual=x)
         xn = layer_norm(x, self.norm1).reshape(B * L, C)
         if inactive(self.drop_path):   # residual adds fused into the proj / fc2 epilogues
             x = self.attn.forward_tokens(xn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
@@ -244,6 +255,19 @@ class Cross_SwinTransformerBlock(nn.Module):
     def forward(self, x, y, x_size):
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
+        if (inactive(self.drop_path_A) and inactive(self.drop_path_B)
+                and ln_linear_ok(x, self.norm1_A, self.attn_A.q) and ln_linear_ok(x, self.norm1_A, self.attn_B.kv)):
+            # norm1 fused into each projection that reads it (x -> q_A, kv_B; y -> q_B, kv_A)
+            qa, xr = ln_linear(x, self.norm1_A, self.attn_A.q, passthrough=True)
+            kvb = ln_linear(x, self.norm1_A, self.attn_B.kv)
+            qb, yr = ln_linear(y, self.norm1_B, self.attn_B.q, passthrough=True)
+            kva = ln_linear(y, self.norm1_B, self.attn_A.kv)
+            xa = self.attn_A.attend(qa.reshape(B * L, C), kva.reshape(B * L, 2 * C), geom,
+                                    residual=xr.reshape(B * L, C)).view(B, L, C)
+            yb = self.attn_B.attend(qb.reshape(B * L, C), kvb.reshape(B * L, 2 * C), geom,
+                                    residual=yr.reshape(B * L, C)).view(B, L, C)
+            return (self.mlp_A(layer_norm(xa, self.norm2_A), residual=xa),
+                    self.mlp_B(layer_norm(yb, self.norm2_B), residual=yb))
         xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
         yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
         if inactive(self.drop_path_A) and inactive(self.drop_path_B):   # fused residual adds

@@ -345,3 +345,82 @@ def test_fused_mlp_weight_grad_is_deterministic(device):
         grads.append([p.grad.clone() for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N", [12, 24, 36])
+@pytest.mark.parametrize("rows,passthrough", [(50003, True), (16, False), (33, True), (7, False)])
+def test_ln_linear_vs_torch_fp64(device, N, rows, passthrough):
+    """norm1 + qkv/q/kv fused (blockops.hip): LN output never stored, backward recomputes it and
+    adds the residual gradient (passthrough) in the same pass."""
+    C = 12
+    gen = torch.Generator().manual_seed(rows * 3 + N)
+    x = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 2 + 0.5
+    gm = torch.randn(C, generator=gen, dtype=torch.float64)
+    bt = torch.randn(C, generator=gen, dtype=torch.float64)
+    w = torch.randn(N, C, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(N, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, N, generator=gen, dtype=torch.float64)
+    gr = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, gm, bt, w, b)]
+    F_ = torch.nn.functional
+    ref = F_.linear(F_.layer_norm(leaves[0], (C,), leaves[1], leaves[2], 1e-5), leaves[3], leaves[4])
+    ((ref * g).sum() + ((leaves[0] * gr).sum() if passthrough else 0)).backward()
+    norm, lin = torch.nn.LayerNorm(C).to(device), torch.nn.Linear(C, N).to(device)
+    with torch.no_grad():
+        norm.weight.copy_(gm.float()); norm.bias.copy_(bt.float())
+        lin.weight.copy_(w.float()); lin.bias.copy_(b.float())
+    xd = x.float().to(device).requires_grad_(True)
+    assert MF.ln_linear_ok(xd, norm, lin)
+    out = MF.ln_linear(xd, norm, lin, passthrough=passthrough)
+    if passthrough:
+        out, xr = out
+        assert xr.data_ptr() == xd.data_ptr()
+        loss = (out * g.float().to(device)).sum() + (xr * gr.float().to(device)).sum()
+    else:
+        loss = (out * g.float().to(device)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    got = [xd.grad, norm.weight.grad, norm.bias.grad, lin.weight.grad, lin.bias.grad]
+    for a, r in zip(got, leaves):
+        assert rel_err(a, r.grad) < TOL
+
+
+def test_ln_linear_grads_are_deterministic(device):
+    C, N, rows = 12, 36, 200003
+    torch.manual_seed(5)
+    norm, lin = torch.nn.LayerNorm(C).to(device), torch.nn.Linear(C, N).to(device)
+    x = torch.randn(rows, C, device=device, requires_grad=True)
+    g = torch.randn(rows, N, device=device)
+    grads = []
+    for _ in range(2):
+        for p in (x, norm.weight, norm.bias, lin.weight, lin.bias):
+            p.grad = None
+        MF.ln_linear(x, norm, lin).backward(g)
+        grads.append([p.grad.clone() for p in (x, norm.weight, norm.bias, lin.weight, lin.bias)])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows", [33, 100003])
+@pytest.mark.parametrize("bias", [True, False])
+def test_linear_bwd_12x12_fused_vs_torch_fp64(device, rows, bias):
+    """attn.proj backward (dx, dW, db in one pass, blockops.hip) through the token Linear."""
+    C = 12
+    gen = torch.Generator().manual_seed(rows + int(bias))
+    x = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    w = torch.randn(C, C, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(C, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    ref = torch.nn.functional.linear(leaves[0], leaves[1], leaves[2] if bias else None)
+    (ref * g).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (x, w, b)]
+    out = MF.linear(dev[0], dev[1], dev[2] if bias else None)
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    for a, r in zip(dev[:2], leaves[:2]):
+        assert rel_err(a.grad, r.grad) < TOL
+    if bias:
+        assert rel_err(dev[2].grad, leaves[2].grad) < TOL
