@@ -215,6 +215,19 @@ int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float* w1, const 
                  const float* w2, const float* dy, float* dx, float* dw1, float* db1, float* dw2,
                  float* db2, void* workspace, void* stream);
 
+/* norm2 + MLP (+ residual) of a pre-norm block in one kernel per direction
+ * (swinfusion_module.py:374-377): y = [x] + fc2(GELU(fc1(LN(x)))), residual_x selecting the
+ * "+ x"; LN statistics are recomputed in the backward (nothing saved).  The backward writes
+ * dx = LN_bwd(dMLP/dLN) (+ dy when residual_x), dgamma, dbeta and the fc gradients.  Same
+ * shapes as mmni_mlp_*; the workspace is mmni_mlp_bwd_workspace_bytes. */
+int mmni_ln_mlp_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
+                    const float* w1, const float* b1, const float* w2, const float* b2, int residual_x, float* y,
+                    void* stream);
+int mmni_ln_mlp_bwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
+                    const float* w1, const float* b1, const float* w2, const float* dy, int residual_x, float* dx,
+                    float* dgamma, float* dbeta, float* dw1, float* db1, float* dw2, float* db2, void* workspace,
+                    void* stream);
+
 /* Fused token ops around the window attention of a SwinFusion block (blockops.hip, C = 12, f32
  * MFMA), replacing norm1 + attn.qkv / attn.q / attn.kv and their backward with the block's
  * residual gradient (swinfusion_module.py:346,121,202-205,377), and the backward of attn.proj

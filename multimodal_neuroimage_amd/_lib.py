@@ -84,6 +84,8 @@ SIGNATURES = {
     "mmni_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 8),
     "mmni_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
     "mmni_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 12),
+    "mmni_ln_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int, _vp, _vp]),
+    "mmni_ln_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int] + [_vp] * 9),
     "mmni_ln_linear_fwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 9),
     "mmni_tok_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(TokDesc)]),
     "mmni_ln_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 15),

@@ -14,6 +14,11 @@
 //             dW2 = dy^T g, dW1 = dpre^T x accumulate over the wave's tiles (24 MFMAs).  Per-wave
 //             partials are summed in a fixed order (column_sum): deterministic.  Reads x and dy,
 //             writes dx.
+// With a LayerNorm prologue (LN template flag) the same kernels compute y = res + MLP(LN(x)),
+// the second half of a pre-norm SwinFusion block (norm2 + mlp + residual,
+// swinfusion_module.py:374-377): the LN statistics are computed in the tile (never stored),
+// the backward recomputes them from x and adds the LN backward, dgamma / dbeta and the residual
+// gradient (res = x) in the same pass.
 // v_mfma_f32_16x16x4_f32 is exact f32 (an fmaf chain per output, cdna_hip_programming.md §FP32-
 // input MFMA) at the f32 VALU rate, and leaves the VALU to the GELU polynomial.
 //
@@ -72,12 +77,34 @@ struct MlpArgs {
     const float* b2;   // (C)
     const float* res;  // (rows, C) contiguous, or null
     float* y;
+    // LayerNorm prologue (LN kernels): x -> (x - mean) * rstd * gamma + beta over the C channels
+    const float* gamma;
+    const float* beta;
+    float eps;
+    int res_x;         // backward: the residual was x itself (dx += dy)
     // backward
     const float* dy;
     float* dx;
     float* partA;      // [waves][H*C + H]  dW1 | db1
     float* partB;      // [waves][C*H + C]  dW2 | db2
+    float* partC;      // [waves][2C]       dgamma | dbeta (LN kernels)
 };
+
+__device__ __forceinline__ float sum_groups(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+// LN statistics of the lane's token from its feature-major channels (nn.LayerNorm: biased
+// variance, eps inside the root); all four lane groups end with the same values.
+__device__ __forceinline__ void ln_stats(const float (&v)[CS], float eps, float& mean, float& rstd) {
+    mean = sum_groups(v[0] + v[1] + v[2]) * (1.0f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int s = 0; s < CS; ++s) q = fmaf(v[s] - mean, v[s] - mean, q);
+    rstd = 1.0f / sqrtf(sum_groups(q) * (1.0f / C) + eps);
+}
 
 // Rows are contiguous 48-byte token rows: a tile's data sits at a wave-uniform base (SGPR) plus a
 // fixed per-lane offset, so every load / store is one instruction with an immediate offset.
@@ -113,6 +140,7 @@ struct TileIO {
     __device__ __forceinline__ bool row_ok(int64_t t0) const { return lg < 3 && t0 + li < rows; }
 };
 
+template <bool LN>
 __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
     const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
     const int64_t wave = __builtin_amdgcn_readfirstlane(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -133,12 +161,24 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) b2c[i] = (lg < 3 && a.b2) ? a.b2[4 * lg + i] : 0.f;
+    float gm[CS], bt[CS];
+#pragma unroll
+    for (int s = 0; s < CS; ++s) {
+        gm[s] = LN ? a.gamma[4 * s + lg] : 1.f;
+        bt[s] = LN ? a.beta[4 * s + lg] : 0.f;
+    }
 
     const int64_t tiles = (a.rows + 15) / 16;
     for (int64_t tile = wave; tile < tiles; tile += nwaves) {
         const int64_t t0 = tile * 16;
         float xb[CS];
         io.load_fm(a.x, t0, xb);
+        if constexpr (LN) {
+            float mean, rstd;
+            ln_stats(xb, a.eps, mean, rstd);
+#pragma unroll
+            for (int s = 0; s < CS; ++s) xb[s] = fmaf((xb[s] - mean) * rstd, gm[s], bt[s]);
+        }
         const bool ok = io.row_ok(t0);
         const int64_t roff = (t0 + li) * C + 4 * lg;
         f4 acc = b2c;
@@ -175,7 +215,9 @@ constexpr int kBwdWaves = 4;   // waves per block (LDS transpose slab per wave)
 #ifndef MMNI_MLP_BWD_OCC
 #define MMNI_MLP_BWD_OCC 3   // min waves per SIMD (caps VGPRs at 168)
 #endif
-__global__ __launch_bounds__(256, MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs a) {
+// (the LN variant carries ~20 more live values: 2 waves per SIMD, no spills)
+template <bool LN>
+__global__ __launch_bounds__(256, LN ? 2 : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs a) {
     __shared__ float tr[kBwdWaves][2][16][H + 4];   // per wave: g and dpre as [token][hidden]
     const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
     const int wib = threadIdx.x >> 6;
@@ -206,6 +248,18 @@ __global__ __launch_bounds__(256, MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs 
         dw2[ht] = (f4){0.f, 0.f, 0.f, 0.f};
         db1[ht] = (f4){0.f, 0.f, 0.f, 0.f};
     }
+    // LN: gamma / beta in the feature-major (s), accumulator-chunk (i) and token-major (li) maps
+    float gm[CS], bt[CS];
+    f4 gm4, dgm = (f4){0.f, 0.f, 0.f, 0.f}, dbt = (f4){0.f, 0.f, 0.f, 0.f};
+    float gml = 0.f, btl = 0.f;
+    if constexpr (LN) {
+#pragma unroll
+        for (int s = 0; s < CS; ++s) { gm[s] = a.gamma[4 * s + lg]; bt[s] = a.beta[4 * s + lg]; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gm4[i] = lg < 3 ? a.gamma[4 * lg + i] : 0.f;
+        gml = li < C ? a.gamma[li] : 0.f;
+        btl = li < C ? a.beta[li] : 0.f;
+    }
     float (*gT)[H + 4] = tr[wib][0];
     float (*dT)[H + 4] = tr[wib][1];
 
@@ -217,6 +271,19 @@ __global__ __launch_bounds__(256, MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs 
         io.load_fm(a.dy, t0, dyb);
         io.load_tm(a.x, t0, xa);
         io.load_tm(a.dy, t0, dya);
+        float mean = 0.f, rstd = 0.f;
+        if constexpr (LN) {
+            // recompute the LN of the tile: feature-major operand, and the token-major copy for
+            // dW1 with the statistics of token 4 s + lg fetched from the lane that owns it
+            ln_stats(xb, a.eps, mean, rstd);
+#pragma unroll
+            for (int s = 0; s < CS; ++s) xb[s] = fmaf((xb[s] - mean) * rstd, gm[s], bt[s]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float ms = __shfl(mean, 4 * s + lg), rs = __shfl(rstd, 4 * s + lg);
+                xa[s] = li < C ? fmaf((xa[s] - ms) * rs, gml, btl) : 0.f;
+            }
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) db2 += dya[s];
         f4 dxo[HT];
@@ -248,7 +315,24 @@ __global__ __launch_bounds__(256, MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs 
             *reinterpret_cast<f4*>(&gT[li][ht * 16 + 4 * lg]) = g;
             *reinterpret_cast<f4*>(&dT[li][ht * 16 + 4 * lg]) = dp;
         }
-        if (io.row_ok(t0)) *reinterpret_cast<f4*>(a.dx + (t0 + li) * C + 4 * lg) = dxo[0] + dxo[1] + dxo[2];
+        if constexpr (LN) {
+            // LN backward on the lane's chunk (channels 4 lg + i of token li) + residual gradient
+            const bool ok = io.row_ok(t0);
+            const int64_t roff = (t0 + li) * C + 4 * lg;
+            const f4 dxn = dxo[0] + dxo[1] + dxo[2];
+            const f4 xc = ok ? *reinterpret_cast<const f4*>(a.x + roff) : (f4){0.f, 0.f, 0.f, 0.f};
+            const f4 xh = ok ? (xc - mean) * rstd : (f4){0.f, 0.f, 0.f, 0.f};
+            const f4 gd = dxn * gm4;
+            const float s1 = sum_groups(gd[0] + gd[1] + gd[2] + gd[3]) * (1.0f / C);
+            const float s2 = sum_groups(gd[0] * xh[0] + gd[1] * xh[1] + gd[2] * xh[2] + gd[3] * xh[3]) * (1.0f / C);
+            f4 dxv = (gd - s1 - xh * s2) * rstd;
+            if (a.res_x && ok) dxv += *reinterpret_cast<const f4*>(a.dy + roff);
+            if (ok) *reinterpret_cast<f4*>(a.dx + roff) = dxv;
+            dgm += dxn * xh;
+            dbt += dxn;
+        } else {
+            if (io.row_ok(t0)) *reinterpret_cast<f4*>(a.dx + (t0 + li) * C + 4 * lg) = dxo[0] + dxo[1] + dxo[2];
+        }
         // weight gradients over the tile's 16 tokens (k-steps of 4 tokens: rows 4 s' + lg)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -284,6 +368,16 @@ __global__ __launch_bounds__(256, MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs 
     db2 += __shfl_xor(db2, 16);
     db2 += __shfl_xor(db2, 32);
     if (lg == 0 && li < C) pb[C * H + li] = db2;
+    if constexpr (LN) {
+        float* pc = a.partC + wave * (2 * C);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float u = dgm[i], v = dbt[i];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) { u += __shfl_xor(u, o); v += __shfl_xor(v, o); }
+            if (li == 0 && lg < 3) { pc[4 * lg + i] = u; pc[C + 4 * lg + i] = v; }
+        }
+    }
 }
 
 }  // namespace mlpk
@@ -297,8 +391,9 @@ static int resident_blocks(const void* kern, int threads, size_t lds) {
     return per_cu * kNumCU;
 }
 
+template <bool LN>
 static int mlp_bwd_waves() {
-    static const int waves = resident_blocks(reinterpret_cast<const void*>(&mlpk::mlp_bwd_kernel),
+    static const int waves = resident_blocks(reinterpret_cast<const void*>(&mlpk::mlp_bwd_kernel<LN>),
                                              64 * mlpk::kBwdWaves, 0) * mlpk::kBwdWaves;
     return waves;
 }
@@ -316,6 +411,16 @@ static int mlp_check(const mmni_mlp_desc* d) {
 
 extern "C" int mmni_mlp_supported(int C, int H) { return C == 12 && H == 48; }
 
+template <bool LN>
+static int mlp_fwd_launch(const mmni_mlp_desc* d, const mlpk::MlpArgs& a, hipStream_t s) {
+    static const int resident = resident_blocks(reinterpret_cast<const void*>(&mlpk::mlp_fwd_kernel<LN>), 256, 0);
+    const int64_t tiles = (d->rows + 15) / 16;
+    int64_t grid = (tiles + 3) / 4;
+    if (grid > resident) grid = resident;
+    mlpk::mlp_fwd_kernel<LN><<<(int)grid, 256, 0, s>>>(a);
+    return launch_status(LN ? "ln_mlp_fwd" : "mlp_fwd");
+}
+
 extern "C" int mmni_mlp_fwd(const mmni_mlp_desc* d, const float* x, const float* w1, const float* b1,
                             const float* w2, const float* b2, const float* residual, float* y, void* stream) {
     int rc = mlp_check(d);
@@ -326,17 +431,44 @@ extern "C" int mmni_mlp_fwd(const mmni_mlp_desc* d, const float* x, const float*
     mlpk::MlpArgs a{};
     a.rows = d->rows;
     a.x = x; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.res = residual; a.y = y;
-    static const int resident = resident_blocks(reinterpret_cast<const void*>(&mlpk::mlp_fwd_kernel), 256, 0);
-    const int64_t tiles = (d->rows + 15) / 16;
-    int64_t grid = (tiles + 3) / 4;
-    if (grid > resident) grid = resident;
-    mlpk::mlp_fwd_kernel<<<(int)grid, 256, 0, (hipStream_t)stream>>>(a);
-    return launch_status("mlp_fwd");
+    return mlp_fwd_launch<false>(d, a, (hipStream_t)stream);
+}
+
+extern "C" int mmni_ln_mlp_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma,
+                               const float* beta, const float* w1, const float* b1, const float* w2, const float* b2,
+                               int residual_x, float* y, void* stream) {
+    int rc = mlp_check(d);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(x && gamma && beta && w1 && w2 && y, "ln_mlp_fwd: null pointer");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
+                   "ln_mlp_fwd: x / y must be 16-byte aligned");
+    mlpk::MlpArgs a{};
+    a.rows = d->rows;
+    a.x = x; a.gamma = gamma; a.beta = beta; a.eps = eps;
+    a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.res = residual_x ? x : nullptr; a.y = y;
+    return mlp_fwd_launch<true>(d, a, (hipStream_t)stream);
 }
 
 extern "C" size_t mmni_mlp_bwd_workspace_bytes(const mmni_mlp_desc* d) {
     if (!d) return 0;
-    return (size_t)mlp_bwd_waves() * ((size_t)d->H * d->C + d->H + (size_t)d->C * d->H + d->C) * sizeof(float);
+    const int waves = mlp_bwd_waves<false>() > mlp_bwd_waves<true>() ? mlp_bwd_waves<false>() : mlp_bwd_waves<true>();
+    return (size_t)waves * ((size_t)d->H * d->C + d->H + (size_t)d->C * d->H + d->C + 2 * (size_t)d->C) * sizeof(float);
+}
+
+template <bool LN>
+static int mlp_bwd_launch(const mmni_mlp_desc* d, mlpk::MlpArgs& a, float* dw1, float* db1, float* dw2, float* db2,
+                          float* dgamma, float* dbeta, void* workspace, hipStream_t s) {
+    const int C = d->C, H = d->H, waves = mlp_bwd_waves<LN>();
+    a.partA = reinterpret_cast<float*>(workspace);
+    a.partB = a.partA + (size_t)waves * (H * C + H);
+    a.partC = a.partB + (size_t)waves * (C * H + C);
+    mlpk::mlp_bwd_kernel<LN><<<waves / mlpk::kBwdWaves, 64 * mlpk::kBwdWaves, 0, s>>>(a);
+    int rc = launch_status(LN ? "ln_mlp_bwd" : "mlp_bwd");
+    if (rc) return rc;
+    column_sum(a.partA, waves, H * C + H, dw1, H * C, db1, s);
+    column_sum(a.partB, waves, C * H + C, dw2, C * H, db2, s);
+    if (LN) column_sum(a.partC, waves, 2 * C, dgamma, C, dbeta, s);
+    return launch_status("mlp_colsum");
 }
 
 extern "C" int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float* w1, const float* b1, const float* w2,
@@ -346,17 +478,25 @@ extern "C" int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float*
     if (rc) return rc;
     MMNI_ARG_CHECK(x && w1 && w2 && dy && dx && dw1 && dw2 && workspace, "mlp_bwd: null pointer");
     MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(dx) % 16 == 0, "mlp_bwd: dx must be 16-byte aligned");
-    const int C = d->C, H = d->H, waves = mlp_bwd_waves();
     mlpk::MlpArgs a{};
     a.rows = d->rows;
     a.x = x; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.dy = dy; a.dx = dx;
-    a.partA = reinterpret_cast<float*>(workspace);
-    a.partB = a.partA + (size_t)waves * (H * C + H);
-    hipStream_t s = (hipStream_t)stream;
-    mlpk::mlp_bwd_kernel<<<waves / mlpk::kBwdWaves, 64 * mlpk::kBwdWaves, 0, s>>>(a);
-    rc = launch_status("mlp_bwd");
+    return mlp_bwd_launch<false>(d, a, dw1, db1, dw2, db2, nullptr, nullptr, workspace, (hipStream_t)stream);
+}
+
+extern "C" int mmni_ln_mlp_bwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma,
+                               const float* beta, const float* w1, const float* b1, const float* w2, const float* dy,
+                               int residual_x, float* dx, float* dgamma, float* dbeta, float* dw1, float* db1,
+                               float* dw2, float* db2, void* workspace, void* stream) {
+    int rc = mlp_check(d);
     if (rc) return rc;
-    column_sum(a.partA, waves, H * C + H, dw1, H * C, db1, s);
-    column_sum(a.partB, waves, C * H + C, dw2, C * H, db2, s);
-    return launch_status("mlp_colsum");
+    MMNI_ARG_CHECK(x && gamma && beta && w1 && w2 && dy && dx && dgamma && dbeta && dw1 && dw2 && workspace,
+                   "ln_mlp_bwd: null pointer");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(dx) % 16 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(dy) % 16 == 0, "ln_mlp_bwd: x / dy / dx must be 16-byte aligned");
+    mlpk::MlpArgs a{};
+    a.rows = d->rows;
+    a.x = x; a.gamma = gamma; a.beta = beta; a.eps = eps; a.res_x = residual_x;
+    a.w1 = w1; a.b1 = b1; a.w2 = w2; a.dy = dy; a.dx = dx;
+    return mlp_bwd_launch<true>(d, a, dw1, db1, dw2, db2, dgamma, dbeta, workspace, (hipStream_t)stream);
 }

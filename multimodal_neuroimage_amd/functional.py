@@ -602,6 +602,73 @@ class _FusedMlp(torch.autograd.Function):
                 dy if ctx.needs_input_grad[5] else None)
 
 
+class _LnMlp(torch.autograd.Function):
+    """x + fc2(GELU(fc1(LN(x)))) (residual_x) or fc2(GELU(fc1(LN(x)))) in one HIP kernel per
+    direction (mlp.hip, LN prologue): the norm2 output, the hidden activation and the LN
+    statistics never reach HBM; the backward adds the LN backward and the residual gradient."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w1, b1, w2, b2, eps, residual_x):
+        H, C = w1.shape
+        x2 = x.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+        d = _mlp_desc(rows, C, H, C, C)
+        ev = KernelTimer.start()
+        check(_lib.load().mmni_ln_mlp_fwd(ctypes.byref(d), float(eps), ptr(x2), ptr(gamma), ptr(beta), ptr(w1), ptr(b1),
+                                          ptr(w2), ptr(b2), int(residual_x), ptr(y), stream_handle(x2.device)),
+              "mmni_ln_mlp_fwd")
+        KernelTimer.stop(f"ln_mlp_fwd_{C}x{H}", ev, 4.0 * rows * C * H, 4.0 * rows * C * 2)
+        ctx.save_for_backward(x2, gamma, beta, w1, b1, w2)
+        ctx.has_b = (b1 is not None, b2 is not None)
+        ctx.eps, ctx.residual_x, ctx.xshape = float(eps), bool(residual_x), x.shape
+        return y.view(*x.shape[:-1], C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gamma, beta, w1, b1, w2 = ctx.saved_tensors
+        H, C = w1.shape
+        dy2 = dy.reshape(-1, C).contiguous()
+        rows = x2.shape[0]
+        dev = x2.device
+        dx = torch.empty(rows, C, device=dev, dtype=torch.float32)
+        dgamma = torch.empty(C, device=dev, dtype=torch.float32)
+        dbeta = torch.empty(C, device=dev, dtype=torch.float32)
+        dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
+        db1 = torch.empty(H, device=dev, dtype=torch.float32)
+        db2 = torch.empty(C, device=dev, dtype=torch.float32)
+        L = _lib.load()
+        d = _mlp_desc(rows, C, H, C, C)
+        ws = torch.empty(L.mmni_mlp_bwd_workspace_bytes(ctypes.byref(d)) // 4, device=dev, dtype=torch.float32)
+        ev = KernelTimer.start()
+        check(L.mmni_ln_mlp_bwd(ctypes.byref(d), ctx.eps, ptr(x2), ptr(gamma), ptr(beta), ptr(w1), ptr(b1), ptr(w2),
+                                ptr(dy2), int(ctx.residual_x), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(dw1), ptr(db1),
+                                ptr(dw2), ptr(db2), ptr(ws), stream_handle(dev)), "mmni_ln_mlp_bwd")
+        KernelTimer.stop(f"ln_mlp_bwd_{C}x{H}", ev, 10.0 * rows * C * H, 4.0 * rows * C * 3)
+        return (dx.view(ctx.xshape), dgamma, dbeta, dw1, db1 if ctx.has_b[0] else None, dw2,
+                db2 if ctx.has_b[1] else None, None, None)
+
+
+def ln_mlp_ok(x, norm, mlp_mod):
+    fc1, fc2 = mlp_mod.fc1, mlp_mod.fc2
+    H, C = fc1.weight.shape
+    return (x.shape[-1] == C and isinstance(norm, torch.nn.LayerNorm) and norm.elementwise_affine
+            and norm.bias is not None and isinstance(mlp_mod.act, torch.nn.GELU) and mlp_mod.act.approximate == "none"
+            and (mlp_mod.drop.p == 0.0 or not mlp_mod.drop.training) and fc2.weight.shape[0] == C
+            and bool(_lib.load().mmni_mlp_supported(C, H)))
+
+
+def ln_mlp(x, norm, mlp_mod, residual_x=True):
+    """[x +] mlp_mod(norm(x)) for an Mlp / Mlp_fusion module (fc1, act, fc2, drop), fused into one
+    kernel per direction when ln_mlp_ok; else LayerNorm + the MLP path."""
+    require_device(x, what="ln_mlp")
+    if ln_mlp_ok(x, norm, mlp_mod):
+        return _LnMlp.apply(x, norm.weight, norm.bias, mlp_mod.fc1.weight, mlp_mod.fc1.bias, mlp_mod.fc2.weight,
+                            mlp_mod.fc2.bias, float(norm.eps), residual_x)
+    return mlp(layer_norm(x, norm), mlp_mod.fc1, mlp_mod.fc2, mlp_mod.act, mlp_mod.drop,
+               residual=x if residual_x else None)
+
+
 def mlp(x, fc1, fc2, act, drop, residual=None):
     """The reference Mlp forward `drop(fc2(drop(act(fc1(x)))))` (+ residual) with the fused HIP
     path when act is exact nn.GELU, the dropouts are inactive and the shapes are compiled; else

@@ -6,7 +6,8 @@ every block is ONE HIP launch (libmmni.so: mmni_wattn_fwd/bwd) that reads the qk
 straight from the un-partitioned channels-last token tensor: the roll, window_partition, mask
 rebuild + H2D copy, bias gather, softmax, AV, window_reverse and reverse roll of the reference
 (swinfusion_module.py:350-373, 114-145) collapse into it.  At C = 12 norm1 is fused into the
-qkv / q / kv projections (blockops.hip) and fc1 + GELU + fc2 is one kernel (mlp.hip).  Every block also accepts 3D token grids (x_size = (D, H, W)), the
+qkv / q / kv projections (blockops.hip) and norm2 + fc1 + GELU + fc2 + residual is one kernel
+per direction (mlp.hip).  Every block also accepts 3D token grids (x_size = (D, H, W)), the
 build's 3D lift; 2D inputs are the D = 1 special case.
 """
 import math
@@ -17,7 +18,7 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
 from ..functional import (window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp, ln_linear,
-                          ln_linear_ok)
+                          ln_linear_ok, ln_mlp)
 from ._common import (DropPath, inactive, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       clamp_window, geometry, patch_merge_gather)
 
@@ -204,7 +205,7 @@ class SwinTransformerBlock_fusion(nn.Module):
             # norm1 + qkv in one kernel; the residual's gradient joins inside its backward
             qkv, xr = ln_linear(x, self.norm1, self.attn.qkv, passthrough=True)
             x = self.attn.attend(qkv.reshape(B * L, 3 * C), geom, residual=xr.reshape(B * L, C)).view(B, L, C)
-            return self.mlp(layer_norm(x, self.norm2), residual=x)
+            return ln_mlp(x, self.norm2, self.mlp)   # x + mlp(norm2(x)), one kernel
         xn = layer_norm(x, self.norm1).reshape(B * L, C)
         if inactive(self.drop_path):   # residual adds fused into the proj / fc2 epilogues
             x = self.attn.forward_tokens(xn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
@@ -266,8 +267,7 @@ class Cross_SwinTransformerBlock(nn.Module):
                                     residual=xr.reshape(B * L, C)).view(B, L, C)
             yb = self.attn_B.attend(qb.reshape(B * L, C), kvb.reshape(B * L, 2 * C), geom,
                                     residual=yr.reshape(B * L, C)).view(B, L, C)
-            return (self.mlp_A(layer_norm(xa, self.norm2_A), residual=xa),
-                    self.mlp_B(layer_norm(yb, self.norm2_B), residual=yb))
+            return ln_mlp(xa, self.norm2_A, self.mlp_A), ln_mlp(yb, self.norm2_B, self.mlp_B)
         xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
         yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
         if inactive(self.drop_path_A) and inactive(self.drop_path_B):   # fused residual adds

@@ -424,3 +424,47 @@ def test_linear_bwd_12x12_fused_vs_torch_fp64(device, rows, bias):
         assert rel_err(a.grad, r.grad) < TOL
     if bias:
         assert rel_err(dev[2].grad, leaves[2].grad) < TOL
+
+
+@pytest.mark.parametrize("rows,residual_x", [(50003, True), (16, False), (33, True), (5, True)])
+def test_ln_mlp_vs_torch_fp64(device, rows, residual_x):
+    """norm2 + fc1 + GELU + fc2 (+ x) in one kernel per direction (mlp.hip LN prologue)."""
+    C, H = 12, 48
+    gen = torch.Generator().manual_seed(rows + 17)
+    x = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 1.5 - 0.3
+    gm = torch.randn(C, generator=gen, dtype=torch.float64)
+    bt = torch.randn(C, generator=gen, dtype=torch.float64)
+    w1 = torch.randn(H, C, generator=gen, dtype=torch.float64) * 0.4
+    b1 = torch.randn(H, generator=gen, dtype=torch.float64) * 0.5
+    w2 = torch.randn(C, H, generator=gen, dtype=torch.float64) * 0.2
+    b2 = torch.randn(C, generator=gen, dtype=torch.float64)
+    g = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    leaves = [t.clone().requires_grad_(True) for t in (x, gm, bt, w1, b1, w2, b2)]
+    F_ = torch.nn.functional
+    xn = F_.layer_norm(leaves[0], (C,), leaves[1], leaves[2], 1e-5)
+    ref = F_.linear(F_.gelu(F_.linear(xn, leaves[3], leaves[4])), leaves[5], leaves[6])
+    if residual_x:
+        ref = ref + leaves[0]
+    (ref * g).sum().backward()
+
+    class _M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1, self.fc2 = torch.nn.Linear(C, H), torch.nn.Linear(H, C)
+            self.act, self.drop = torch.nn.GELU(), torch.nn.Dropout(0.0)
+
+    m, norm = _M().to(device), torch.nn.LayerNorm(C).to(device)
+    with torch.no_grad():
+        norm.weight.copy_(gm.float()); norm.bias.copy_(bt.float())
+        m.fc1.weight.copy_(w1.float()); m.fc1.bias.copy_(b1.float())
+        m.fc2.weight.copy_(w2.float()); m.fc2.bias.copy_(b2.float())
+    xd = x.float().to(device).requires_grad_(True)
+    assert MF.ln_mlp_ok(xd, norm, m)
+    out = MF.ln_mlp(xd, norm, m, residual_x=residual_x)
+    (out * g.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    got = [xd.grad, norm.weight.grad, norm.bias.grad, m.fc1.weight.grad, m.fc1.bias.grad, m.fc2.weight.grad,
+           m.fc2.bias.grad]
+    for a, r in zip(got, leaves):
+        assert rel_err(a, r.grad) < TOL
