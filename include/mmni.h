@@ -253,6 +253,31 @@ int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, 
 int mmni_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* w,
                     float* dx, float* dw, float* db, void* workspace, void* stream);
 
+/* Input preprocessing (preprocess.hip), replacing the per-subject host work
+ * of the reference's Dataset.__getitem__:
+ *   zscore          y = (x - mean) / std over each of n_arrays contiguous arrays of `count`
+ *                   floats (scipy.stats.zscore(axis=None), ddof 0; datasets.py:416, 664), statistics
+ *                   in double, deterministic; half_round != 0 rounds through float16 (.half()).
+ *   fir_highpass    host: nitime FilterAnalyzer.fir high-pass taps (firwin hamming, spectral
+ *                   inversion), cutoff as a fraction of Nyquist.
+ *   fmri_band_split y (B, R, Lmax) series with lens[b] valid samples (device int32) ->
+ *                   raw / low / ultralow (B, seq, R): zscore(x), zscore(fir(x)), zscore(x - fir(x))
+ *                   over time, zero-padded to seq with (seq - L) / 2 in front (datasets.py:665-698).
+ *                   fir = zero-phase filtfilt (odd extension 3 * ntaps) with the mean restored.
+ *                   Needs 3 * ntaps < lens[b] <= Lmax <= seq <= 1024, ntaps odd <= 129. */
+typedef struct mmni_bandsplit_desc {
+    int32_t B, R;      /* subjects, ROIs */
+    int32_t Lmax;      /* row stride of y (time samples) */
+    int32_t seq;       /* padded output length (368 in the reference) */
+    int32_t ntaps;     /* FIR length (nitime filt_order + 1 = 65) */
+} mmni_bandsplit_desc;
+size_t mmni_zscore_workspace_bytes(int64_t n_arrays);
+int mmni_zscore(int64_t n_arrays, int64_t count, const float* x, float* y, int half_round, void* workspace,
+                void* stream);
+int mmni_fir_highpass_taps(int ntaps, double cutoff_frac, double* taps);
+int mmni_fmri_band_split(const mmni_bandsplit_desc* d, const float* y, const int32_t* lens, const double* taps,
+                         float* raw, float* low, float* ultralow, void* stream);
+
 int mmni_version(void);
 const char* mmni_last_error(void);
 

@@ -58,6 +58,10 @@ class TokDesc(ctypes.Structure):
     _fields_ = [("rows", _c_i64), ("C", _c_i32), ("N", _c_i32), ("eps", _c_f)]
 
 
+class BandSplitDesc(ctypes.Structure):
+    _fields_ = [("B", _c_i32), ("R", _c_i32), ("Lmax", _c_i32), ("seq", _c_i32), ("ntaps", _c_i32)]
+
+
 # symbol -> (restype, argtypes); every symbol include/mmni.h declares
 SIGNATURES = {
     "mmni_version": (_c_int, []),
@@ -86,6 +90,10 @@ SIGNATURES = {
     "mmni_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 12),
     "mmni_ln_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int, _vp, _vp]),
     "mmni_ln_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int] + [_vp] * 9),
+    "mmni_zscore_workspace_bytes": (ctypes.c_size_t, [_c_i64]),
+    "mmni_zscore": (_c_int, [_c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp]),
+    "mmni_fir_highpass_taps": (_c_int, [_c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
+    "mmni_fmri_band_split": (_c_int, [ctypes.POINTER(BandSplitDesc)] + [_vp] * 7),
     "mmni_ln_linear_fwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 9),
     "mmni_tok_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(TokDesc)]),
     "mmni_ln_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 15),
