@@ -103,3 +103,39 @@ def test_single_process_env_is_a_no_op():
     m = nn.Linear(2, 2)
     assert D.wrap_ddp(m, env) is m
     assert D.max_over_ranks(3.5, env) == 3.5
+
+
+def _writer_worker(rank, world, port, out):
+    from multimodal_neuroimage_amd.trainer import Writer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    env = D.init_from_env(backend="gloo")
+    w = Writer(["train", "val"], 0.5, env=env, fine_tune_task="binary_classification")
+    g = torch.Generator().manual_seed(7)
+    logits = torch.randn(12, generator=g)
+    truth = (torch.arange(12) % 3 == 0).float()
+    mine = [i for i in range(12) if i % world == rank]          # each rank validates its shard
+    w.record("val", torch.tensor(mine), logits[mine], truth[mine])
+    for k in range(2):
+        w.write_losses({"binary_classification": torch.tensor(0.5 + rank + k), "total": torch.tensor(0.5 + rank + k)},
+                       "val")
+    w.loss_summary(lr=0)
+    w.accuracy_summary(mid_epoch=False)
+    out[rank] = dict(metrics=w.current_metrics, loss=w.total_val_loss_history[-1])
+    D.shutdown(env)
+
+
+def test_writer_gathers_predictions_over_ranks():
+    """Validation metrics are computed over ALL ranks' subjects (the reference computes them per
+    rank on its shard), and the loss summary is the mean over ranks."""
+    from multimodal_neuroimage_amd.metrics import classification_metrics
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_writer_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    g = torch.Generator().manual_seed(7)
+    logits = torch.randn(12, generator=g)
+    truth = (torch.arange(12) % 3 == 0).float()
+    ref = classification_metrics(truth.tolist(), torch.sigmoid(logits).tolist(), "val", 0.5)
+    for r in range(world):
+        assert out[r]["metrics"] == pytest.approx(ref, rel=1e-6)
+        assert out[r]["loss"] == pytest.approx(1.5)     # mean of rank 0 (0.5, 1.5) and rank 1 (1.5, 2.5)
