@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 1
+#define MMNI_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -77,21 +77,25 @@ typedef struct mmni_wattn_desc {
 int mmni_wattn_fwd(const mmni_wattn_desc* d,
                    const float* q, const float* k, const float* v,
                    const float* table, const float* tau,
-                   float* out, float* lse, void* stream);
+                   float* out, float* lse, unsigned int* vmax, void* stream);
 
 /* Backward (flash-style recompute from lse).  dq/dk/dv are fully overwritten (every token
  * belongs to exactly one window).  dtable (Tsz, heads) and dtau (heads) are ACCUMULATED
  * (dtable += grad): the caller zeroes them.  dtau may be NULL for kind 0.
  * workspace: >= mmni_wattn_bwd_workspace_bytes(d) bytes, 8-byte aligned, contents ignored
  * (the library zeroes it on the stream); it holds the 64-bit fixed-point table gradient, which
- * makes dtable bitwise deterministic. */
+ * makes dtable bitwise deterministic.
+ * vmax (both calls, nullable): one uint32 the caller zeroes before the forward; the forward raises
+ * it to the float bits of max|v| over the call (folded into the K/V staging), and the backward
+ * then scans only dout for the fixed-point bound instead of dout and v.  ABI v2 added it. */
 size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d);
 int mmni_wattn_bwd(const mmni_wattn_desc* d,
                    const float* q, const float* k, const float* v,
                    const float* table, const float* tau,
                    const float* out, const float* dout, const float* lse,
                    float* dq, float* dk, float* dv,
-                   float* dtable, float* dtau, void* workspace, void* stream);
+                   float* dtable, float* dtau, void* workspace, const unsigned int* vmax,
+                   void* stream);
 
 /* Integer maps the attention kernels use, exported for bit-exact parity tests (row a0).
  *   mmni_window_rows:   rows[w*N + t] = source token row of window-local token t of window w

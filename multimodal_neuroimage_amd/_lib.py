@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -66,8 +66,8 @@ class BandSplitDesc(ctypes.Structure):
 SIGNATURES = {
     "mmni_version": (_c_int, []),
     "mmni_last_error": (ctypes.c_char_p, []),
-    "mmni_wattn_fwd": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 15),
+    "mmni_wattn_fwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 9),
+    "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 16),
     "mmni_wattn_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WAttnDesc)]),
     "mmni_window_rows": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
     "mmni_window_mask": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),

@@ -138,6 +138,119 @@ __global__ __launch_bounds__(256) void conv3d_dx_kernel(ConvArgs a) {
     for (int ci = 0; ci < CIN; ++ci) a.dx[e * CIN + ci] = acc[ci];
 }
 
+// ------------------------------------------------------------------------------------
+// k = 3, stride 1, pad 1 (the a4b convs): LDS-tiled stencil for the forward and dx
+// ------------------------------------------------------------------------------------
+// One workgroup = an 8 x 8 x 4 tile of output voxels (one per lane).  The tile's input halo
+// (10 x 10 x 6 rows of NI channels) is staged in LDS once, so each input row is read from HBM
+// ~1.7x instead of once per tap through L2 (the gather kernels above re-read 19-21 GB per dx
+// launch at 96^3).  Weights are wave-uniform (scalar loads).
+//   MODE 0 (forward):  out[v][o] = bias[o] + sum_t sum_i x[v + t - 1][i] * w[o][i][t], LeakyReLU
+//   MODE 1 (dx):       dx[v][i]  = sum_t sum_o dz[v + 1 - t][o] * w[o][i][t],
+//                      dz = dy * LeakyReLU'(y) computed once per halo row while staging.
+constexpr int kTX = 8, kTY = 8, kTZ = 4;
+constexpr int kHX = kTX + 2, kHY = kTY + 2, kHZ = kTZ + 2;
+
+// LDS row stride of NI floats: whole float4 chunks, an odd number of them (bank spread)
+template <int NI>
+struct HaloRow {
+    static constexpr int kChunks0 = (NI + 3) / 4;
+    static constexpr int kChunks = NI < 4 ? 0 : (kChunks0 % 2 ? kChunks0 : kChunks0 + 1);
+    static constexpr int kStride = NI < 4 ? NI : kChunks * 4;
+};
+
+template <int CIN, int COUT, int MODE>
+__global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
+    constexpr int NI = MODE == 0 ? CIN : COUT;   // channels of the staged operand
+    constexpr int NO = MODE == 0 ? COUT : CIN;   // channels of the result
+    constexpr int RS = HaloRow<NI>::kStride;
+    __shared__ __attribute__((aligned(16))) float halo[kHX * kHY * kHZ * RS];
+    const int ntx = (a.W + kTX - 1) / kTX, nty = (a.H + kTY - 1) / kTY, ntz = (a.D + kTZ - 1) / kTZ;
+    int tile = blockIdx.x;
+    const int bx = tile % ntx; tile /= ntx;
+    const int by = tile % nty; tile /= nty;
+    const int bz = tile % ntz;
+    const int b = tile / ntz;
+    const int x0 = bx * kTX - 1, y0 = by * kTY - 1, z0 = bz * kTZ - 1;
+    const float* src = MODE == 0 ? a.x : a.dy;
+    // ---- stage the halo (zero outside the volume)
+    for (int e = threadIdx.x; e < kHX * kHY * kHZ; e += 256) {
+        const int hx = e % kHX, hy = (e / kHX) % kHY, hz = e / (kHX * kHY);
+        const int gx = x0 + hx, gy = y0 + hy, gz = z0 + hz;
+        float v[NI];
+        const bool in = gx >= 0 && gx < a.W && gy >= 0 && gy < a.H && gz >= 0 && gz < a.D;
+        const int64_t row = in ? (((int64_t)b * a.D + gz) * a.H + gy) * a.W + gx : 0;
+#pragma unroll
+        for (int c = 0; c < NI; ++c) v[c] = in ? src[row * NI + c] : 0.f;
+        if (MODE == 1 && in && a.slope != 1.f) {
+#pragma unroll
+            for (int c = 0; c < NI; ++c) v[c] *= lrelu_grad(a.y[row * NI + c], a.slope);
+        }
+        float* dst = halo + e * RS;
+        if constexpr (RS % 4 == 0) {
+#pragma unroll
+            for (int c = 0; c < RS; c += 4)
+                *reinterpret_cast<float4*>(dst + c) = make_float4(c < NI ? v[c] : 0.f, c + 1 < NI ? v[c + 1] : 0.f,
+                                                                  c + 2 < NI ? v[c + 2] : 0.f, c + 3 < NI ? v[c + 3] : 0.f);
+        } else {
+#pragma unroll
+            for (int c = 0; c < NI; ++c) dst[c] = v[c];
+        }
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 7, ty = (threadIdx.x >> 3) & 7, tz = threadIdx.x >> 6;
+    float acc[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[o] = (MODE == 0 && a.bias) ? a.bias[o] : 0.f;
+    for (int t = 0; t < 27; ++t) {
+        const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
+        // forward reads x[v + k - 1] = halo[v_local + k]; dx reads dz[v + 1 - k] = halo[v_local + 2 - k]
+        const int hz = MODE == 0 ? tz + kz : tz + 2 - kz;
+        const int hy = MODE == 0 ? ty + ky : ty + 2 - ky;
+        const int hx = MODE == 0 ? tx + kx : tx + 2 - kx;
+        const float* r = halo + ((hz * kHY + hy) * kHX + hx) * RS;
+        float v[NI];
+        if constexpr (RS % 4 == 0) {
+#pragma unroll
+            for (int c = 0; c < NI; c += 4) {
+                const float4 q = *reinterpret_cast<const float4*>(r + c);
+                v[c] = q.x;
+                if (c + 1 < NI) v[c + 1] = q.y;
+                if (c + 2 < NI) v[c + 2] = q.z;
+                if (c + 3 < NI) v[c + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NI; ++c) v[c] = r[c];
+        }
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            float sacc = acc[o];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const float wv = MODE == 0 ? a.w[(o * CIN + i) * 27 + t] : a.w[(i * CIN + o) * 27 + t];
+                sacc = fmaf(v[i], wv, sacc);
+            }
+            acc[o] = sacc;
+        }
+    }
+    const int gx = bx * kTX + tx, gy = by * kTY + ty, gz = bz * kTZ + tz;
+    if (gx >= a.W || gy >= a.H || gz >= a.D) return;
+    const int64_t vox = (((int64_t)b * a.D + gz) * a.H + gy) * a.W + gx;
+    float* out = (MODE == 0 ? a.y : a.dx) + vox * NO;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) out[o] = MODE == 0 ? (acc[o] > 0.f ? acc[o] : acc[o] * a.slope) : acc[o];
+}
+
+__host__ __forceinline__ bool is_k3_same(const ConvArgs& a) {
+    return a.kd == 3 && a.kh == 3 && a.kw == 3 && a.sd == 1 && a.sh == 1 && a.sw == 1 && a.pd == 1 && a.ph == 1 &&
+           a.pw == 1 && a.Do == a.D && a.Ho == a.H && a.Wo == a.W;
+}
+
+__host__ __forceinline__ unsigned k3_tiles(const ConvArgs& a) {
+    return (unsigned)((int64_t)a.B * ((a.D + kTZ - 1) / kTZ) * ((a.H + kTY - 1) / kTY) * ((a.W + kTX - 1) / kTX));
+}
+
 // dW[co][ci][t] += sum_u dz[u][co] * x[in(u,t)][ci];  db[co] += sum_u dz[u][co]
 template <int CIN, int COUT, int MAXP>
 __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
@@ -158,6 +271,9 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
 #pragma unroll
     for (int co = 0; co < COUT; ++co) dbacc[co] = 0.f;
     const int tiles_per_b = a.ntz * a.nty * a.ntx;
+    const int G = MAXP == 1 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;   // lane groups over voxels
+    const int gi = MAXP == 1 ? tid / npairs : 0;
+    const int pl = MAXP == 1 ? tid - gi * npairs : tid;
 
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         int rr = tile;
@@ -197,21 +313,22 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             x_s[e] = xv;
         }
         __syncthreads();
-        // pair (t, ci) owned by this lane: p = tid + m*256
-        for (int u = 0; u < Tout; ++u) {
+        // pair (t, ci) owned by this lane: p = tid + m*256; with fewer pairs than lanes (MAXP 1)
+        // the block splits into G groups of npairs lanes that take every G-th output voxel
+        for (int u = gi; u < Tout; u += G) {
             const int ux = u % a.TX, uy = (u / a.TX) % a.TY, uz = u / (a.TX * a.TY);
             float g[COUT];
 #pragma unroll
             for (int co = 0; co < COUT; ++co) g[co] = dz_s[u * COUT + co];
-            if (tid < COUT) {
+            if (pl < COUT && gi < G) {
 #pragma unroll
                 for (int co = 0; co < COUT; ++co)
-                    if (co == tid) dbacc[co] += g[co];
+                    if (co == pl) dbacc[co] += g[co];
             }
 #pragma unroll
             for (int m = 0; m < MAXP; ++m) {
-                const int p = tid + m * 256;
-                if (p < npairs) {
+                const int p = pl + m * 256;
+                if (p < npairs && gi < G) {
                     const int ci = p % CIN, t = p / CIN;
                     const int tx = t % a.kw, ty = (t / a.kw) % a.kh, tz = t / (a.kw * a.kh);
                     const int hv = ((uz * a.sd + tz) * a.HY + (uy * a.sh + ty)) * a.HX + (ux * a.sw + tx);
@@ -224,17 +341,17 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int m = 0; m < MAXP; ++m) {
-        const int p = tid + m * 256;
-        if (p < npairs) {
+        const int p = pl + m * 256;
+        if (p < npairs && gi < G) {
             const int ci = p % CIN, t = p / CIN;
 #pragma unroll
             for (int co = 0; co < COUT; ++co) atomicAdd(&a.dw[((int64_t)co * CIN + ci) * K3 + t], acc[m][co]);
         }
     }
-    if (a.db && tid < COUT) {
+    if (a.db && pl < COUT && gi < G) {
 #pragma unroll
         for (int co = 0; co < COUT; ++co)
-            if (co == tid) atomicAdd(&a.db[co], dbacc[co]);
+            if (co == pl) atomicAdd(&a.db[co], dbacc[co]);
     }
 }
 
@@ -258,6 +375,12 @@ static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
 
 template <int CIN, int COUT>
 static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
+    // measured at 96^3 (r05): the LDS tile wins for CIN <= 12 with >= 6 outputs, or CIN <= 3; the
+    // lane-per-voxel gather is faster for 24 -> 12 (tile LDS 67 KB: 2 blocks/CU) and 6 -> 3
+    if (is_k3_same(a) && ((CIN <= 12 && COUT >= 6) || CIN <= 3)) {
+        conv3d_k3_tile_kernel<CIN, COUT, 0><<<k3_tiles(a), 256, 0, s>>>(a);
+        return launch_status("conv3d_fwd_k3");
+    }
     const int64_t n = (int64_t)a.B * a.Do * a.Ho * a.Wo;
     conv3d_fwd_kernel<CIN, COUT><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
     return launch_status("conv3d_fwd");
@@ -265,7 +388,11 @@ static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
 
 template <int CIN, int COUT>
 static int conv_bwd_launch(ConvArgs& a, hipStream_t s) {
-    if (a.dx) {
+    if (a.dx && is_k3_same(a)) {
+        conv3d_k3_tile_kernel<CIN, COUT, 1><<<k3_tiles(a), 256, 0, s>>>(a);
+        int rc = launch_status("conv3d_dx_k3");
+        if (rc) return rc;
+    } else if (a.dx) {
         const int64_t n = (int64_t)a.B * a.D * a.H * a.W;
         conv3d_dx_kernel<CIN, COUT><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
         int rc = launch_status("conv3d_dx");

@@ -31,7 +31,8 @@
 
 namespace mmni {
 
-// max|dout| and max|v| for the fixed-point bound (non-negative float bits order as uints)
+// max|dout| and max|v| for the fixed-point bound (non-negative float bits order as uints).
+// dout == nullptr: v only; v == nullptr: dout only.
 __global__ void wattn_absmax_kernel(const float* dout, long long os, const float* v, long long vs, long long T,
                                     int C, unsigned int* maxbits) {
     float md = 0.f, mv = 0.f;
@@ -39,17 +40,31 @@ __global__ void wattn_absmax_kernel(const float* dout, long long os, const float
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const long long r = i / C;
         const int c = (int)(i - r * C);
-        md = fmaxf(md, fabsf(dout[r * os + c]));
-        mv = fmaxf(mv, fabsf(v[r * vs + c]));
+        if (dout) md = fmaxf(md, fabsf(dout[r * os + c]));
+        if (v) mv = fmaxf(mv, fabsf(v[r * vs + c]));
     }
     for (int o = 32; o > 0; o >>= 1) {
         md = fmaxf(md, __shfl_xor(md, o));
         mv = fmaxf(mv, __shfl_xor(mv, o));
     }
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(&maxbits[0], __float_as_uint(md));
-        atomicMax(&maxbits[1], __float_as_uint(mv));
+        if (dout) atomicMax(&maxbits[0], __float_as_uint(md));
+        if (v) atomicMax(&maxbits[1], __float_as_uint(mv));
     }
+}
+
+// max|dout| over a contiguous, 16-byte aligned array of n4 float4 (the common case: dout rows of
+// C % 4 == 0 floats, stride C), and max|v| taken from the forward's running maximum (vmax).
+__global__ __launch_bounds__(256) void wattn_absmax_dout4_kernel(const float4* dout, long long n4,
+                                                                 const unsigned int* vmax, unsigned int* maxbits) {
+    float md = 0.f;
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const float4 x = dout[i];
+        md = fmaxf(md, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    }
+    for (int o = 32; o > 0; o >>= 1) md = fmaxf(md, __shfl_xor(md, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(&maxbits[0], __float_as_uint(md));
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&maxbits[1], *vmax);
 }
 
 // ------------------------------------------------------------------------------------
@@ -481,9 +496,9 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
 }
 
 __global__ void wattn_dtable_convert_kernel(const unsigned long long* fix, const unsigned int* maxbits, int hd,
-                                            float* dtable, int n) {
+                                            int shift, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dtable[e] += (float)ldexp((double)(long long)fix[e], -fix_exponent(maxbits, hd));
+    if (e < n) dtable[e] += (float)ldexp((double)(long long)fix[e], -(fix_exponent(maxbits, hd) - shift));
 }
 
 // ------------------------------------------------------------------------------------
@@ -568,7 +583,8 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
     const size_t T = (size_t)WPB * NPAD;
     if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
     if (packed)
-        return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * ((NH + 3) & ~3) * 4 + (size_t)Tsz * (NH + 1) * 8 +
+        return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * ((NH + 3) & ~3) * 4 +
+               (size_t)Tsz * (NH + kDtabPad) * (kDtab32 ? 4 : 8) +
                (size_t)NH * 4;
     const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
     return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
@@ -667,7 +683,8 @@ static bool row_aligned(const void* p, int64_t stride, int C) {
 using namespace mmni;
 
 extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
-                              const float* table, const float* tau, float* out, float* lse, void* stream) {
+                              const float* table, const float* tau, float* out, float* lse, unsigned int* vmax,
+                              void* stream) {
     WAArgs a{};
     int HD = 0;
     int rc = fill_args(d, a, HD);
@@ -687,11 +704,17 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
+    a.vmax = packed ? vmax : nullptr;   // the packed kernels fold max|v| into their K/V staging
     rc = ensure_lds_attr(kf, cfg.lds);
     if (rc) return rc;
     void* args[] = {&a};
     hipError_t e = hipLaunchKernel(kf, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_fwd launch: %s", hipGetErrorString(e)); return (int)e; }
+    if (vmax && !packed) {   // generic kernels: a separate pass over v (vmax is maxbits[1]-shaped: pass vmax - 1)
+        const long long T = (long long)a.g.nwin * a.g.N;
+        wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(nullptr, 0, v, d->v_stride, T, d->C, vmax - 1);
+        return launch_status("wattn_absmax_v");
+    }
     return 0;
 }
 
@@ -704,7 +727,7 @@ extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
 extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
                               const float* table, const float* tau, const float* out, const float* dout,
                               const float* lse, float* dq, float* dk, float* dv, float* dtable, float* dtau,
-                              void* workspace, void* stream) {
+                              void* workspace, const unsigned int* vmax, void* stream) {
     WAArgs a{};
     int HD = 0;
     int rc = fill_args(d, a, HD);
@@ -730,6 +753,16 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;
     a.dtab_fix = reinterpret_cast<unsigned long long*>(workspace);
+    a.fix_shift = 0;
+    if (packed && kDtab32) {
+        // contributions to one table entry per head and block: at most one per query of each window
+        // the block handles; each is < 2^(30 - shift) after scaling, so the 32-bit sum needs
+        // 2^shift >= windows_per_block * N / 2
+        const int64_t per_block = (int64_t)((cfg.ngroups + cfg.grid - 1) / cfg.grid) * cfg.WPB * a.g.N;
+        int sh = 0;
+        while ((int64_t(1) << (sh + 1)) < per_block) ++sh;
+        a.fix_shift = sh;
+    }
     rc = ensure_lds_attr(kb, cfg.lds);
     if (rc) return rc;
     const int ntab = a.g.Tsz * d->heads;
@@ -737,14 +770,23 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8 + 16, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
     const long long T = (long long)a.g.nwin * a.g.N;   // tokens
-    wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C, a.maxbits);
+    if (vmax && d->o_stride == d->C && d->C % 4 == 0 && reinterpret_cast<uintptr_t>(dout) % 16 == 0) {
+        const long long n4 = T * d->C / 4;
+        long long blocks = (n4 + 255) / 256;
+        if (blocks > 2048) blocks = 2048;
+        wattn_absmax_dout4_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+            reinterpret_cast<const float4*>(dout), n4, vmax, a.maxbits);
+    } else {
+        wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C,
+                                                                   a.maxbits);
+    }
     rc = launch_status("wattn_absmax");
     if (rc) return rc;
     void* args[] = {&a};
     e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
     wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD,
-                                                                                     dtable, ntab);
+                                                                                     a.fix_shift, dtable, ntab);
     return launch_status("wattn_dtable_convert");
 }
 

@@ -72,6 +72,8 @@ struct WAArgs {
     float* dtau;
     unsigned long long* dtab_fix;   // global int64 fixed-point accumulator (workspace)
     unsigned int* maxbits;          // workspace tail: max|dout|, max|v| bits (fixed-point scale)
+    int fix_shift;                  // bits the block-local fixed-point scale is lowered by (32-bit LDS sums)
+    unsigned int* vmax;             // forward (packed kernels): running max|v| (float bits), or null
 };
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
@@ -80,6 +82,18 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK_CHUNK
 #define MMNI_PK_CHUNK 6
 #endif
+#ifndef MMNI_DTAB_PAD
+#define MMNI_DTAB_PAD 1
+#endif
+#ifndef MMNI_TAB_SWZ
+#define MMNI_TAB_SWZ 1
+#endif
+#ifndef MMNI_DTAB32
+#define MMNI_DTAB32 0
+#endif
+constexpr int kDtabPad = MMNI_DTAB_PAD;   // packed bwd: table-gradient row stride NH + pad (u64)
+constexpr int kTabSwz = MMNI_TAB_SWZ;     // packed bwd: float4 chunks of table row r XOR-ed with (r >> 3)
+constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local table-gradient sums
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.

@@ -15,6 +15,8 @@
 // permuted into it when staged, dq/dk/dv/out are permuted back before the store.
 #include "wattn_common.h"
 
+#include <type_traits>
+
 // Kernel ablations for experiments only (scripts/build_variant.sh): bit 0 drops the table-gradient
 // atomics, bit 1 the pass-B loop, bit 2 the pass-A loop.  Product builds use 0.
 #ifndef MMNI_ABL
@@ -109,6 +111,7 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
     for (int P = 0; P < NP; ++P)
         tau2[P] = (KIND == 1) ? (f2){a.tau[2 * P], a.tau[2 * P + 1]} * kLog2e : splat(a.scale * kLog2e);
 
+    float vabs = 0.f;   // running max|v| of the rows this thread staged (for the backward's bound)
     for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
         for (int e = tid; e < WPB * NPAD; e += blockDim.x) {
             const int w2 = e / NPAD, t2 = e - w2 * NPAD;
@@ -119,6 +122,8 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
                 const TokenInfo ti = token_info(g, w, t2);
                 load_row<C>(kr, a.k + ti.row * a.ks);
                 load_row<C>(vr, a.v + ti.row * a.vs);
+#pragma unroll
+                for (int c = 0; c < C; ++c) vabs = fmaxf(vabs, fabsf(vr[c]));
                 if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
                 mt = make_int2(ti.code | (ti.rc << 16), 0);
             } else {
@@ -237,6 +242,10 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
         }
         __syncthreads();
     }
+    if (a.vmax != nullptr) {
+        for (int o = 32; o > 0; o >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, o));
+        if ((tid & 63) == 0) atomicMax(a.vmax, __float_as_uint(vabs));
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -284,13 +293,22 @@ __device__ __forceinline__ void lds_row(f2 (&d)[C / 2], const float* s) {
     }
 }
 
+// position of float h of table row `row` (NHP floats per row, float4 chunks optionally swizzled)
+template <int NHP>
+__device__ __forceinline__ int tab_pos(int row, int h) {
+    constexpr int NCH = NHP / 4;   // float4 chunks per row; the swizzle needs a power of two
+    const int c = h >> 2;
+    const int cs = (kTabSwz && (NCH & (NCH - 1)) == 0) ? (c ^ ((row >> 3) & (NCH - 1))) : c;
+    return row * NHP + cs * 4 + (h & 3);
+}
+
 // table row (NHP floats, NHP % 4 == 0) -> NP float2
 template <int NP, int NHP>
-__device__ __forceinline__ void lds_tab(f2 (&d)[NP], const float* s) {
+__device__ __forceinline__ void lds_tab(f2 (&d)[NP], const float* tab, int row) {
     float t[NHP];
 #pragma unroll
     for (int i = 0; i < NHP; i += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(s + i);
+        const float4 x = *reinterpret_cast<const float4*>(tab + tab_pos<NHP>(row, i));
         t[i] = x.x; t[i + 1] = x.y; t[i + 2] = x.z; t[i + 3] = x.w;
     }
 #pragma unroll
@@ -301,7 +319,10 @@ template <int C, int KIND, int MAXT>
 __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     constexpr int HD = 2, NH = C / HD, NP = NH / 2;
     constexpr int NHP = (NH + 3) & ~3;   // table row stride (float4 reads)
-    constexpr int DS = NH + 1;           // table-gradient row stride in u64 (odd: spreads LDS banks)
+    constexpr int DS = NH + kDtabPad;    // table-gradient row stride in words (odd: spreads LDS banks)
+    // block-local table-gradient sums: 64-bit, or 32-bit with the fixed-point scale lowered by
+    // fix_shift bits so that every block's sums fit (host: 2^fix_shift >= windows per block * N / 2)
+    using dt_t = std::conditional_t<kDtab32, unsigned int, unsigned long long>;
     static_assert(NH % 2 == 0, "head pairs");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WGeom& g = a.g;
@@ -311,7 +332,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     float* rs_s = smem + (size_t)T * 2 * C;               // [T][2NH]: pass B lse2 | -delta*2^S (pk pairs)
     int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)T * 2 * NH);
     float* tab_s = reinterpret_cast<float*>(meta_s + T);  // [Tsz][NHP], log2-domain bias
-    unsigned long long* dtab_s = reinterpret_cast<unsigned long long*>(tab_s + (size_t)g.Tsz * NHP);
+    dt_t* dtab_s = reinterpret_cast<dt_t*>(tab_s + (size_t)g.Tsz * NHP);
     float* dtau_s = reinterpret_cast<float*>(dtab_s + (size_t)g.Tsz * DS);
 
     const int tid = threadIdx.x;
@@ -322,11 +343,11 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
 
     for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
         const int row = e / NHP, h = e - row * NHP;
-        tab_s[e] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
+        tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
     }
-    for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0ull;
+    for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0;
     if (tid < NH) dtau_s[tid] = 0.f;
-    const int fexp = fix_exponent(a.maxbits, HD);
+    const int fexp = fix_exponent(a.maxbits, HD) - a.fix_shift;
     const float fs = exp2f((float)fexp);       // 2^S
     const float ifs = exp2f((float)-fexp);     // 2^-S (exact)
     f2 dtr[NP];
@@ -417,7 +438,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
             const int jb = p * nk;
             int2 mm = mw[jb];
             // deferred table-gradient atomics of the previous key (issued after this key's reads)
-            unsigned long long* dtp = dtab_s;
+            dt_t* dtp = dtab_s;
             long long fx[NH];
 #pragma unroll
             for (int h = 0; h < NH; ++h) fx[h] = 0;
@@ -426,12 +447,12 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                 const int2 mnext = mw[j + 1];   // prefetch (reads past the slice on the last key: unused)
                 const int tix = cq - (mm.x & 0xffff);
                 f2 tb[NP], kj[C / 2], vj[C / 2];
-                lds_tab<NP, NHP>(tb, tab_s + tix * NHP);
+                lds_tab<NP, NHP>(tb, tab_s, tix);
                 lds_row<C>(kj, kvw + (size_t)j * 2 * C);
                 lds_row<C>(vj, kvw + (size_t)j * 2 * C + C);
 #pragma unroll
                 for (int h = 0; h < NH; ++h)
-                    if (!(MMNI_ABL & 1)) atomicAdd(&dtp[h], (unsigned long long)fx[h]);
+                    if (!(MMNI_ABL & 1)) atomicAdd(&dtp[h], (dt_t)fx[h]);
                 dtp = dtab_s + tix * DS;
                 f2 base[NP];
                 if (masked) {
@@ -469,7 +490,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                 mm = mnext;
             }
 #pragma unroll
-            for (int h = 0; h < NH; ++h) atomicAdd(&dtp[h], (unsigned long long)fx[h]);
+            for (int h = 0; h < NH; ++h) atomicAdd(&dtp[h], (dt_t)fx[h]);
             for (int o = 1; o < KS; o <<= 1) {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) dqa[i] += shfl2(dqa[i], o);
@@ -546,7 +567,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
                 const int i = ib + n;
                 const int2 mnext = mw[i + 1];
                 f2 tb[NP], ai[C / 2], gi[C / 2];
-                lds_tab<NP, NHP>(tb, tab_s + ((mm.x & 0xffff) + cko) * NHP);
+                lds_tab<NP, NHP>(tb, tab_s, (mm.x & 0xffff) + cko);
                 lds_row<C>(ai, qdw + (size_t)i * 2 * C);
                 lds_row<C>(gi, qdw + (size_t)i * 2 * C + C);
                 const f2* rsi = reinterpret_cast<const f2*>(rsw + (size_t)i * 2 * NH);
@@ -618,8 +639,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     }
     __syncthreads();
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
-        const unsigned long long v = dtab_s[(e / NH) * DS + e % NH];
-        if (v != 0ull) atomicAdd(&a.dtab_fix[e], v);
+        const dt_t v = dtab_s[(e / NH) * DS + e % NH];
+        if (v != 0) atomicAdd(&a.dtab_fix[e], kDtab32 ? (unsigned long long)(long long)(int)v : (unsigned long long)v);
     }
     if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] * ifs / (a.tau[tid] * kLog2e));
 }

@@ -144,18 +144,19 @@ class _WindowAttention(torch.autograd.Function):
         v = kv_src[:, v_off:]
         d = _wattn_desc(geom, C, heads, kind, scale, q.stride(0), k.stride(0), v.stride(0), C)
         L = _lib.load()
+        vmax = torch.zeros(1, device=q_src.device, dtype=torch.int32)   # max|v| bits for the bwd bound
         ev = KernelTimer.start()
-        check(L.mmni_wattn_fwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau_c), ptr(out), ptr(lse),
+        check(L.mmni_wattn_fwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau_c), ptr(out), ptr(lse), ptr(vmax),
                                stream_handle(q_src.device)), "mmni_wattn_fwd")
         # SURVEY §8d counting: fwd 4*T*N*C FLOPs, 4*T*C*4 bytes (q, k, v read, o written)
         KernelTimer.stop(f"wattn_fwd_k{kind}_C{C}_N{geom.N}", ev, 4.0 * rows * geom.N * C, 16.0 * rows * C)
-        ctx.save_for_backward(q_src, kv_src, table, tau_c, out, lse)
+        ctx.save_for_backward(q_src, kv_src, table, tau_c, out, lse, vmax)
         ctx.cfg = (geom, heads, kind, scale, k_off, v_off, packed, C)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q_src, kv_src, table, tau, out, lse = ctx.saved_tensors
+        q_src, kv_src, table, tau, out, lse, vmax = ctx.saved_tensors
         geom, heads, kind, scale, k_off, v_off, packed, C = ctx.cfg
         dout = dout.contiguous()
         if packed:
@@ -175,7 +176,7 @@ class _WindowAttention(torch.autograd.Function):
         ws = torch.empty(L.mmni_wattn_bwd_workspace_bytes(d) // 8, device=q_src.device, dtype=torch.int64)
         ev = KernelTimer.start()
         check(L.mmni_wattn_bwd(d, ptr(q), ptr(k), ptr(v), ptr(table), ptr(tau), ptr(out), ptr(dout), ptr(lse),
-                               ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau), ptr(ws),
+                               ptr(dq), ptr(dk), ptr(dv), ptr(dtable), ptr(dtau), ptr(ws), ptr(vmax),
                                stream_handle(q_src.device)), "mmni_wattn_bwd")
         # SURVEY §8d counting: bwd 10*T*N*C FLOPs; bytes 8*T*C*4 + 4*T*heads (lse)
         rows = q_src.shape[0]

@@ -52,7 +52,7 @@ def test_wattn_rejects_bad_descriptors(bad, msg):
     lib = _lib.load()
     d = _wdesc(**bad)
     dummy = ctypes.c_void_p(16)
-    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None)
+    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None, None)
     assert rc < 0
     assert msg in lib.mmni_last_error().decode()
 
@@ -61,7 +61,7 @@ def test_wattn_rejects_unsupported_head_dim():
     lib = _lib.load()
     d = _wdesc(C=20, heads=2, q_stride=60, k_stride=60, v_stride=60, o_stride=20)
     dummy = ctypes.c_void_p(16)
-    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None)
+    rc = lib.mmni_wattn_fwd(d, dummy, dummy, dummy, dummy, dummy, dummy, dummy, None, None)
     assert rc == -2
     assert "unsupported" in lib.mmni_last_error().decode()
 
