@@ -590,15 +590,16 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
     return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
 }
 
-static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg) {
-    const int chunk = packed ? kPkChunk : CH;
-    const int N = g.N;
-    int KS = N >= 128 ? 4 : (N >= 32 ? 2 : 1);
+// qpl: queries per lane (2 for wattn_fwd_pk2_kernel): a window occupies N / qpl x KS lanes.
+static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
+    const int chunk = packed ? (qpl == 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
+    const int N = g.N, R = N / qpl;
+    int KS = qpl == 2 ? MMNI_PK2_KS : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
-    while (KS > 1 && r64(N * KS) > maxt) KS >>= 1;
-    MMNI_ARG_CHECK(r64(N) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
+    while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
+    MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
-    int WPB = target / (N * KS);
+    int WPB = target / (R * KS);
     if (WPB < 1) WPB = 1;
     const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
@@ -607,7 +608,7 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     cfg.KS = KS;
     cfg.WPB = WPB;
     cfg.NPAD = NPAD;
-    cfg.threads = r64(WPB * N * KS);
+    cfg.threads = r64(WPB * R * KS);
     cfg.ngroups = (g.nwin + WPB - 1) / WPB;
     int per_cu = (int)((160 * 1024) / lds);
     const int by_threads = 2048 / cfg.threads;
@@ -623,12 +624,15 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     return 0;
 }
 
-static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed) {
+static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
+                    int& qpl) {
     const int C = d->C;
     packed = false;
-    int mf = 0, mb = 0;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, kf, kb, mf, mb)) {
+    qpl = 1;
+    int mf = 0, mb = 0, qf = 1;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf)) {
         maxt = bwd ? mb : mf;
+        qpl = bwd ? 1 : qf;
         packed = true;
         return 0;
     }
@@ -697,10 +701,11 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    rc = dispatch(d, HD, false, kf, kb, maxt, packed);
+    int qpl = 1;
+    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg, qpl);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
@@ -744,7 +749,8 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    rc = dispatch(d, HD, true, kf, kb, maxt, packed);
+    int qpl = 1;
+    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
     WAConfig cfg;
     rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg);

@@ -88,6 +88,15 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_TAB_SWZ
 #define MMNI_TAB_SWZ 1
 #endif
+#ifndef MMNI_FWD_QPL
+#define MMNI_FWD_QPL 2        // queries per lane of the packed C = 12 forward
+#endif
+#ifndef MMNI_PK2_CHUNK
+#define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
+#endif
+#ifndef MMNI_PK2_KS
+#define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
+#endif
 #ifndef MMNI_DTAB32
 #define MMNI_DTAB32 0
 #endif
@@ -97,7 +106,7 @@ constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local tabl
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
-int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b);
+int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the

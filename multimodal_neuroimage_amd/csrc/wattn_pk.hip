@@ -249,6 +249,200 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
 }
 
 // ------------------------------------------------------------------------------------
+// forward, two queries per lane
+// ------------------------------------------------------------------------------------
+// The forward above is bound by LDS instructions, not VALU: per (query, key) a lane reads the key
+// row (3 x b128), the value row (3 x b128), the bias-table row and the key metadata, and a
+// broadcast ds_read_b128 costs the same LDS cycles as a scattered one.  Here each lane carries
+// queries t and t + N/2 of its window against the same keys, so every K/V/metadata read serves
+// two queries (LDS instructions per query-key pair 8.5 -> 5).  Lanes per window: N/2 x KS.
+template <int C, int KIND, int MAXT>
+__global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
+    constexpr int HD = 2, NH = C / HD, NP = NH / 2, CK = MMNI_PK2_CHUNK;
+    static_assert(NH % 2 == 0, "head pairs");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB, NHALF = N / 2;
+    float* kv_s = smem;                                              // [WPB*NPAD][2C] pk k | pk v
+    int2* meta_s = reinterpret_cast<int2*>(kv_s + (size_t)WPB * NPAD * 2 * C);  // [WPB*NPAD]
+    float* tab_s = reinterpret_cast<float*>(meta_s + WPB * NPAD);     // [Tsz][NH]
+
+    const int tid = threadIdx.x;
+    const int r = tid / KS, p = tid - r * KS;
+    const int wl = r / NHALF, t = r - wl * NHALF;
+    const int wl_c = wl < WPB ? wl : WPB - 1;
+
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+
+    f2 tau2[NP];
+#pragma unroll
+    for (int P = 0; P < NP; ++P)
+        tau2[P] = (KIND == 1) ? (f2){a.tau[2 * P], a.tau[2 * P + 1]} * kLog2e : splat(a.scale * kLog2e);
+
+    float vabs = 0.f;
+    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+        for (int e = tid; e < WPB * NPAD; e += blockDim.x) {
+            const int w2 = e / NPAD, t2 = e - w2 * NPAD;
+            const int w = grp * WPB + w2;
+            float kr[C], vr[C];
+            int2 mt;
+            if (t2 < N && w < g.nwin) {
+                const TokenInfo ti = token_info(g, w, t2);
+                load_row<C>(kr, a.k + ti.row * a.ks);
+                load_row<C>(vr, a.v + ti.row * a.vs);
+#pragma unroll
+                for (int c = 0; c < C; ++c) vabs = fmaxf(vabs, fabsf(vr[c]));
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
+                mt = make_int2(ti.code | (ti.rc << 16), 0);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) { kr[c] = 0.f; vr[c] = 0.f; }
+                mt = make_int2(0, __float_as_int(-INFINITY));
+            }
+            f2 kp[C / 2], vp[C / 2];
+            pack_row<C>(kp, kr);
+            pack_row<C>(vp, vr);
+            store_pk<C>(kv_s + (size_t)e * 2 * C, kp);
+            store_pk<C>(kv_s + (size_t)e * 2 * C + C, vp);
+            meta_s[e] = mt;
+        }
+
+        const int w = grp * WPB + wl;
+        const bool active = (wl < WPB) && (w < g.nwin);
+        f2 q[2][C / 2];
+        int cq[2] = {0, 0}, rq[2] = {0, 0};
+        int64_t row[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float qr[C];
+            if (active) {
+                const TokenInfo ti = token_info(g, w, t + u * NHALF);
+                row[u] = ti.row;
+                cq[u] = ti.code + g.off;
+                rq[u] = ti.rc;
+                load_row<C>(qr, a.q + ti.row * a.qs);
+                if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(qr, nrm); }
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) qr[c] = 0.f;
+            }
+            pack_row<C>(q[u], qr);
+#pragma unroll
+            for (int P = 0; P < NP; ++P) { q[u][2 * P] *= tau2[P]; q[u][2 * P + 1] *= tau2[P]; }
+        }
+        __syncthreads();
+
+        f2 m[2][NP], l[2][NP], acc[2][C / 2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int P = 0; P < NP; ++P) { m[u][P] = splat(-INFINITY); l[u][P] = splat(0.f); }
+#pragma unroll
+            for (int i = 0; i < C / 2; ++i) acc[u][i] = splat(0.f);
+        }
+
+        const float* kvw = kv_s + (size_t)wl_c * NPAD * 2 * C;
+        const int2* mw = meta_s + wl_c * NPAD;
+        const int nk = NPAD / KS;
+        for (int n = 0; n < nk; n += CK) {
+            f2 s[2][CK][NP];
+#pragma unroll
+            for (int cc = 0; cc < CK; ++cc) {
+                const int j = p + KS * (n + cc);
+                const int2 mt = mw[j];
+                const int code = mt.x & 0xffff, rcj = mt.x >> 16;
+                const f2* kr = reinterpret_cast<const f2*>(kvw + (size_t)j * 2 * C);
+                f2 kk[C / 2];
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) kk[i] = kr[i];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const float madd = (rcj == rq[u] ? 0.f : kMask2) + __int_as_float(mt.y);
+                    const f2* tb = reinterpret_cast<const f2*>(tab_s + (cq[u] - code) * NH);
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) {
+                        f2 d = tb[P] + splat(madd);
+                        d = pfma(q[u][2 * P], kk[2 * P], d);
+                        s[u][cc][P] = pfma(q[u][2 * P + 1], kk[2 * P + 1], d);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int P = 0; P < NP; ++P) {
+                    f2 cm = s[u][0][P];
+#pragma unroll
+                    for (int cc = 1; cc < CK; ++cc) cm = max2(cm, s[u][cc][P]);
+                    const f2 mn = max2(m[u][P], cm);
+                    const f2 al = exp2_2(m[u][P] - mn);
+                    m[u][P] = mn;
+                    l[u][P] *= al;
+                    acc[u][2 * P] *= al;
+                    acc[u][2 * P + 1] *= al;
+                }
+            }
+#pragma unroll
+            for (int cc = 0; cc < CK; ++cc) {
+                const int j = p + KS * (n + cc);
+                const f2* vr = reinterpret_cast<const f2*>(kvw + (size_t)j * 2 * C + C);
+                f2 vv[C / 2];
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) vv[i] = vr[i];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) {
+                        const f2 pj = exp2_2(s[u][cc][P] - m[u][P]);
+                        l[u][P] += pj;
+                        acc[u][2 * P] = pfma(pj, vv[2 * P], acc[u][2 * P]);
+                        acc[u][2 * P + 1] = pfma(pj, vv[2 * P + 1], acc[u][2 * P + 1]);
+                    }
+                }
+            }
+        }
+        for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int P = 0; P < NP; ++P) {
+                    const f2 mo = shfl2(m[u][P], o), lo = shfl2(l[u][P], o);
+                    const f2 mn = max2(m[u][P], mo);
+                    const f2 fa = exp2_2(m[u][P] - mn), fb = exp2_2(mo - mn);
+                    l[u][P] = l[u][P] * fa + lo * fb;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        acc[u][2 * P + c] = acc[u][2 * P + c] * fa + shfl2(acc[u][2 * P + c], o) * fb;
+                    m[u][P] = mn;
+                }
+            }
+        }
+        if (active && p == 0) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f2 op[C / 2];
+#pragma unroll
+                for (int P = 0; P < NP; ++P) {
+                    const f2 inv = (f2){1.0f / l[u][P].x, 1.0f / l[u][P].y};
+                    op[2 * P] = acc[u][2 * P] * inv;
+                    op[2 * P + 1] = acc[u][2 * P + 1] * inv;
+                    a.lse[row[u] * NH + 2 * P] = (m[u][P].x + fast_log2(l[u][P].x)) * kLn2;
+                    a.lse[row[u] * NH + 2 * P + 1] = (m[u][P].y + fast_log2(l[u][P].y)) * kLn2;
+                }
+                float o[C];
+                unpack_row<C>(o, op);
+                store_row<C>(a.out + row[u] * a.os, o);
+            }
+        }
+        __syncthreads();
+    }
+    if (a.vmax != nullptr) {
+        for (int o = 32; o > 0; o >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, o));
+        if ((tid & 63) == 0) atomicMax(a.vmax, __float_as_uint(vabs));
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------
 // Same two-pass flash-style structure as wattn_bwd_kernel (pass A: lane = query row -> dq and
@@ -656,12 +850,24 @@ static void* pk_bwd(int kind) {
                 : reinterpret_cast<void*>(&wattn_bwd_pk_kernel<C, 0, MAXT>);
 }
 
+template <int C, int MAXT>
+static void* pk2_fwd(int kind) {
+    return kind ? reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 1, MAXT>)
+                : reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 0, MAXT>);
+}
+
 // Forward blocks of <= 512 threads (KS = 2 at N = 216): two blocks share a CU, so one block's
 // K/V gather overlaps the other's compute.  The backward's LDS (bias table + its 64-bit
 // gradient) allows one block per CU; it keeps 1024 threads (KS = 4) for occupancy.
-int wattn_pk_kernels(int C, int kind, void*& kf, void*& kb, int& maxt_f, int& maxt_b) {
-    if (C == 12) { kf = pk_fwd<12, 512>(kind); kb = pk_bwd<12, 1024>(kind); maxt_f = 512; maxt_b = 1024; return 1; }
-    if (C == 24) { kf = pk_fwd<24, 512>(kind); kb = pk_bwd<24, 512>(kind); maxt_f = 512; maxt_b = 512; return 1; }
+// qpl_f: queries per lane of the forward (2: wattn_fwd_pk2_kernel, windows of even N).
+int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f) {
+    const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
+    qpl_f = two ? 2 : 1;
+    if (C == 12) {
+        kf = two ? pk2_fwd<12, 512>(kind) : pk_fwd<12, 512>(kind);
+        kb = pk_bwd<12, 1024>(kind); maxt_f = 512; maxt_b = 1024; return 1;
+    }
+    if (C == 24) { kf = pk_fwd<24, 512>(kind); kb = pk_bwd<24, 512>(kind); maxt_f = 512; maxt_b = 512; qpl_f = 1; return 1; }
     return 0;
 }
 
