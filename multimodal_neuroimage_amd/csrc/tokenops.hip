@@ -117,43 +117,71 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t rows, const 
     }
 }
 
-// out[j] = sum_b part[b][j] in a fixed order (columns j >= split go to out2[j - split]) (deterministic for a given nparts): a block owns CW
-// columns, its 1024 threads split the rows into RG = 1024 / CW interleaved groups with four
-// independent double accumulators each, then the groups are combined in order through LDS.
+// out[j] = sum_b part[b][j] in a fixed order (columns j >= split go to out2[j - split]);
+// deterministic for a given nparts.  Two stages so that the grid is wide (the per-wave partial
+// slabs are ~2k rows x <= 1k columns; one block per 64 columns left most of the GPU idle):
+//   stage 1  block (column group, row slice): CW columns x rps rows, RG = 1024 / CW interleaved
+//            row groups with four double accumulators each, combined in order through LDS; the
+//            double result is split into hi + lo floats stored IN PLACE in the slice's first two
+//            rows (same column: no other block reads them);
+//   stage 2  one lane per column adds the slices' (hi + lo) in slice order, in double.
 template <int CW>
-__global__ __launch_bounds__(1024) void column_sum_kernel(const float* __restrict__ part, int nparts, int ncols,
-                                                          float* __restrict__ out, int split,
-                                                          float* __restrict__ out2) {
+__global__ __launch_bounds__(1024) void column_sum_stage1_kernel(float* __restrict__ part, int nparts, int ncols,
+                                                                 int rps) {
     constexpr int RG = 1024 / CW;
     __shared__ double red[RG][CW];
     const int tx = threadIdx.x % CW, ty = threadIdx.x / CW;
     const int j = blockIdx.x * CW + tx;
+    const int r0 = blockIdx.y * rps;
+    const int r1 = r0 + rps < nparts ? r0 + rps : nparts;
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     if (j < ncols) {
-        int b = ty;
-        for (; b + 3 * RG < nparts; b += 4 * RG) {
+        int b = r0 + ty;
+        for (; b + 3 * RG < r1; b += 4 * RG) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) s[u] += part[(int64_t)(b + u * RG) * ncols + j];
         }
-        for (int u = 0; b < nparts; b += RG, ++u) s[u & 3] += part[(int64_t)b * ncols + j];
+        for (int u = 0; b < r1; b += RG, ++u) s[u & 3] += part[(int64_t)b * ncols + j];
     }
     red[ty][tx] = (s[0] + s[1]) + (s[2] + s[3]);
     __syncthreads();
     if (ty == 0 && j < ncols) {
         double t = 0.0;
         for (int g = 0; g < RG; ++g) t += red[g][tx];
-        if (j < split) out[j] = (float)t;
-        else if (out2) out2[j - split] = (float)t;
+        const float hi = (float)t;
+        part[(int64_t)r0 * ncols + j] = hi;
+        if (r1 - r0 > 1) part[(int64_t)(r0 + 1) * ncols + j] = (float)(t - (double)hi);
     }
 }
 
-void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
+__global__ __launch_bounds__(256) void column_sum_stage2_kernel(const float* __restrict__ part, int nparts, int ncols,
+                                                                int rps, int nslices, float* __restrict__ out,
+                                                                int split, float* __restrict__ out2) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= ncols) return;
+    double t = 0.0;
+    for (int sl = 0; sl < nslices; ++sl) {
+        const int r0 = sl * rps;
+        t += (double)part[(int64_t)r0 * ncols + j];
+        if (nparts - r0 > 1) t += (double)part[(int64_t)(r0 + 1) * ncols + j];
+    }
+    if (j < split) out[j] = (float)t;
+    else if (out2) out2[j - split] = (float)t;
+}
+
+void column_sum(const float* part_c, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
+    float* part = const_cast<float*>(part_c);   // scratch: stage 1 leaves its sums in place
+    const int want = 16;                        // row slices
+    int rps = (nparts + want - 1) / want;
+    if (rps < 2) rps = 2;
+    const int nslices = (nparts + rps - 1) / rps;
     if (ncols <= 16)
-        column_sum_kernel<16><<<(ncols + 15) / 16, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
+        column_sum_stage1_kernel<16><<<dim3((ncols + 15) / 16, nslices), 1024, 0, s>>>(part, nparts, ncols, rps);
     else if (ncols <= 32)
-        column_sum_kernel<32><<<(ncols + 31) / 32, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
+        column_sum_stage1_kernel<32><<<dim3((ncols + 31) / 32, nslices), 1024, 0, s>>>(part, nparts, ncols, rps);
     else
-        column_sum_kernel<64><<<(ncols + 63) / 64, 1024, 0, s>>>(part, nparts, ncols, out, split, out2);
+        column_sum_stage1_kernel<64><<<dim3((ncols + 63) / 64, nslices), 1024, 0, s>>>(part, nparts, ncols, rps);
+    column_sum_stage2_kernel<<<(ncols + 255) / 256, 256, 0, s>>>(part, nparts, ncols, rps, nslices, out, split, out2);
 }
 
 using f4 = __attribute__((ext_vector_type(4))) float;

@@ -55,16 +55,24 @@ __global__ void wattn_absmax_kernel(const float* dout, long long os, const float
 
 // max|dout| over a contiguous, 16-byte aligned array of n4 float4 (the common case: dout rows of
 // C % 4 == 0 floats, stride C), and max|v| taken from the forward's running maximum (vmax).
-__global__ __launch_bounds__(256) void wattn_absmax_dout4_kernel(const float4* dout, long long n4,
-                                                                 const unsigned int* vmax, unsigned int* maxbits) {
+// (One same-address atomic per block: per-wave atomics on one word serialise at the L2 and
+// cost ~60 us at 8k waves.)
+__global__ __launch_bounds__(1024) void wattn_absmax_dout4_kernel(const float4* dout, long long n4,
+                                                                  const unsigned int* vmax, unsigned int* maxbits) {
+    __shared__ float red[16];
     float md = 0.f;
-    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    for (long long i = blockIdx.x * 1024ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 1024) {
         const float4 x = dout[i];
         md = fmaxf(md, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     }
     for (int o = 32; o > 0; o >>= 1) md = fmaxf(md, __shfl_xor(md, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(&maxbits[0], __float_as_uint(md));
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&maxbits[1], *vmax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = md;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) md = fmaxf(md, red[w]);
+        atomicMax(&maxbits[0], __float_as_uint(md));
+        if (blockIdx.x == 0) atomicMax(&maxbits[1], *vmax);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -778,9 +786,9 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     const long long T = (long long)a.g.nwin * a.g.N;   // tokens
     if (vmax && d->o_stride == d->C && d->C % 4 == 0 && reinterpret_cast<uintptr_t>(dout) % 16 == 0) {
         const long long n4 = T * d->C / 4;
-        long long blocks = (n4 + 255) / 256;
-        if (blocks > 2048) blocks = 2048;
-        wattn_absmax_dout4_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+        long long blocks = (n4 + 1023) / 1024;
+        if (blocks > 512) blocks = 512;
+        wattn_absmax_dout4_kernel<<<(unsigned)blocks, 1024, 0, (hipStream_t)stream>>>(
             reinterpret_cast<const float4*>(dout), n4, vmax, a.maxbits);
     } else {
         wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C,

@@ -23,7 +23,7 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_kernel<(\d+), (\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(4)}_C{m.group(2)}"
-    m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk_kernel<(\d+), (\d), \d+>", name)
+    m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk2?_kernel<(\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
@@ -38,9 +38,18 @@ def bench_key(name):
     m = re.search(r"mmni::linear_dw_kernel<(\d+), (\d+)>", name)
     if m:
         return f"linear_dw_tiles{m.group(1)}x{m.group(2)}"
+    m = re.search(r"mmni::mlpk::(mlp_fwd|mlp_bwd)_kernel<(true|false)>", name)
+    if m:
+        return f"{'ln_' if m.group(2) == 'true' else ''}{m.group(1)}_12x48"
     m = re.search(r"mmni::mlpk::(mlp_fwd|mlp_bwd)_kernel", name)
     if m:
         return f"{m.group(1)}_12x48"
+    m = re.search(r"mmni::blk::(ln_linear_fwd|ln_linear_bwd)_kernel<(\d+)>", name)
+    if m:
+        return f"{m.group(1)}_12x{m.group(2)}"
+    m = re.search(r"mmni::blk::linear_bwd_kernel", name)
+    if m:
+        return "linear_bwd_12x12"
     m = re.search(r"mmni::token_linear_kernel<(\d+), (\d+), (\d), \d+>", name)
     if m:
         return f"token_linear_e{m.group(3)}_{m.group(1)}x{m.group(2)}"
