@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=["c3"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c4"],
+                    help="c3: SwinFusion 3D (default, the BASELINE metric's config); c4: SwinCrossmodal3D composite")
     ap.add_argument("--batch", type=int, default=4, help="volume pairs per GPU")
     ap.add_argument("--size", type=int, default=96, help="volume side (voxels)")
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
@@ -52,6 +53,17 @@ def model_kwargs(size):
     return dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
                 attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=size, patch_size=8,
                 window_size=6, no_init_weights=True, volume_size=size)
+
+
+def c4_kwargs(size):
+    """SURVEY §8d C4 composite: Swin-V2 stage 1 per modality (12^3 tokens at 96^3 / patch 8), 2 cross
+    blocks, Linear(12 -> 84), the crossmodal head with 12 layers / 12 heads / causal mask on
+    1,728-token sequences; dropouts 0 (the reference's default attention dropout 0.1 is RNG-only)."""
+    return dict(fine_tune_task="binary_classification", volume_size=size, patch_size=8, swin_embed_dim=12,
+                window_size=6, swin_heads=3, cross_heads=6, swin_depth=2, mlp_ratio=4.0, intermediate_vec=84,
+                num_heads_mult=12, nlevels=12, attn_dropout=0.0, attn_dropout_u=0.0, relu_dropout=0.0,
+                res_dropout=0.0, embed_dropout=0.0, out_dropout=0.0, attn_mask=True, mixing="U2L_and_L2U",
+                concat_method="concat", fmri_type="divided_frequency")
 
 
 def synthetic_pairs(n, size, device, seed):
@@ -78,6 +90,27 @@ def latest_pmc(kernel_name):
             if kernel_name.startswith(k + "_") and v.get("hbm_bytes_per_launch") is not None:
                 return v["hbm_bytes_per_launch"], os.path.basename(f)
     return None, None
+
+
+def cpu_baseline_c4(size):
+    """Oracle composite (fp32 CPU) fwd+bwd on one pair at the full size: the crossmodal head's cost
+    does not scale with a smaller volume in a simple way, so no sampling."""
+    from multimodal_neuroimage_amd import model as M
+    from oracle import model as OM   # cpu_baseline leg: the oracle is the timed CPU port
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = M.SwinCrossmodal3D(**c4_kwargs(size))
+    p = OM.params_of(m, torch.float32)
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(1, size, size, size, generator=g)
+    B = torch.randn(1, size, size, size, generator=g)
+    cfg = dict(patch=8, window_size=6, swin_heads=3, cross_heads=6, depth=2, layers=12, heads=12)
+    t0 = time.perf_counter()
+    out = OM.swin_crossmodal_logits(p, A, B, cfg)
+    torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out)).backward()
+    t = time.perf_counter() - t0
+    return dict(value=round(1.0 / t, 6), unit="volume-pairs/s", cores=threads, kind="port",
+                sample=f"oracle SwinCrossmodal3D fwd+bwd, 1 pair at {size}^3 ({t:.1f} s); fp32")
 
 
 def cpu_baseline(size, sample):
@@ -120,8 +153,11 @@ def main():
     from multimodal_neuroimage_amd import model as M
     from multimodal_neuroimage_amd.functional import KernelTimer
 
-    kw = model_kwargs(args.size)
-    model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
+    if args.config == "c4":
+        model = D.wrap_ddp(M.SwinCrossmodal3D(use_checkpoint=args.checkpoint, **c4_kwargs(args.size)).to(device), env)
+    else:
+        kw = model_kwargs(args.size)
+        model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank)
     lossf = torch.nn.BCEWithLogitsLoss()
@@ -172,16 +208,22 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.size, args.cpu_sample_size)
+                cpu = cpu_baseline_c4(args.size) if args.config == "c4" else cpu_baseline(args.size,
+                                                                                          args.cpu_sample_size)
             except Exception as e:  # the baseline is reported, never required
                 cpu = dict(error=str(e))
         line = dict(metric=METRIC, value=round(value, 4), unit="volume-pairs/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms, 2), higher_is_better=True, scaling="weak",
                     vs_baseline=None, dtype="f32", data="synthetic (z-scored N(0,1) volumes, Bernoulli labels)",
-                    config=dict(workload=f"C3: SwinFusion 3D lift, {args.size}^3 sMRI+fMRI pairs",
-                                global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
-                                patch=8, window=6, tokens_per_volume=args.size ** 3,
-                                parallelism=f"dp{world}", checkpoint=args.checkpoint),
+                    config=(dict(workload=f"C3: SwinFusion 3D lift, {args.size}^3 sMRI+fMRI pairs",
+                                 global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
+                                 patch=8, window=6, tokens_per_volume=args.size ** 3,
+                                 parallelism=f"dp{world}", checkpoint=args.checkpoint) if args.config == "c3" else
+                            dict(workload=f"C4: SwinCrossmodal3D composite, {args.size}^3 pairs, crossmodal head "
+                                          f"12 layers x 12 heads on {(args.size // 8) ** 3}-token sequences",
+                                 global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
+                                 patch=8, window=6, sequence=(args.size // 8) ** 3, parallelism=f"dp{world}",
+                                 checkpoint=args.checkpoint)),
                     roofline=roofline, cpu_baseline=cpu, loss=round(loss_v, 5),
                     kernels={k: dict(launches=v["launches"], avg_ms=round(v["avg_ms"], 4),
                                      total_ms=round(v["total_ms"], 2)) for k, v in kern.items()},

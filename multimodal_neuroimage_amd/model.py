@@ -503,3 +503,66 @@ class Transformer_Net_Cross_Attention(BaseModel):
             out_cls = self.trans_u_mem(h_u_with_ls)[-1]
         pred = self.out_layer2(out_cls)
         return {'embedding_per_ROIs': out_cls, self.task: pred}
+
+
+class SwinCrossmodal3D(BaseModel):
+    """Build-defined C4 composite (the reference's Func_Struct_Cross,
+    model.py:1948-2020, is not instantiable, so its topology is composed from the hot-path modules):
+
+        per modality   PatchEmbed Conv3d(k=s=patch) + LN -> Swin-V2 stage 1 (BasicLayer, 2 blocks,
+                       swin heads, window ws; swin_v2_module.py:425-433)
+        fusion         Cross_BasicLayer (2 Cross_SwinTransformerBlocks, cross_heads;
+                       swinfusion_module.py:698-747)
+        to sequences   Linear(embed -> intermediate_vec) per modality: (B, L, d) token sequences
+        head           the crossmodal topology of Transformer_Net_Cross_Attention
+                       (model.py:489-537: l<-u and u<-l encoders, concat, trans_mem, last token,
+                       out_layer1/2; nlevels layers, num_heads_mult heads, causal mask) on the
+                       L = (volume / patch)^3 token sequences, feature_map_gen 'no'.
+    forward(A, B): two (B, D, H, W) volumes -> {'embedding_per_ROIs', fine_tune_task: (B, 1)}.
+    """
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        self.task = kwargs.get('fine_tune_task')
+        self.volume_size = kwargs.get('volume_size') or 96
+        self.patch_size = kwargs.get('patch_size') or 8
+        self.embed_dim = kwargs.get('swin_embed_dim') or 12
+        ws = kwargs.get('window_size') or 6
+        swin_heads = kwargs.get('swin_heads') or 3
+        cross_heads = kwargs.get('cross_heads') or 6
+        depth = kwargs.get('swin_depth') or 2
+        mlp_ratio = kwargs.get('mlp_ratio') or 4.0
+        d = kwargs.get('intermediate_vec') or 84
+        use_ckpt = bool(kwargs.get('use_checkpoint', False))
+        V, P, E = self.volume_size, self.patch_size, self.embed_dim
+
+        def embed():
+            return PatchEmbed(img_size_w=V, img_size_h=V, patch_size=P, in_chans=1, embed_dim=E,
+                              norm_layer=nn.LayerNorm, img_size_d=V)
+
+        self.patch_embed_A, self.patch_embed_B = embed(), embed()
+        res = tuple(self.patch_embed_A.patches_resolution)
+        self.patches_resolution = res
+
+        def stage():
+            return BasicLayer(dim=E, input_resolution=res, depth=depth, num_heads_swin=swin_heads, window_size=ws,
+                              mlp_ratio=mlp_ratio, qkv_bias=True, drop=0.0, attn_drop=0.0, drop_path=0.0,
+                              norm_layer=nn.LayerNorm, downsample=None, use_checkpoint=use_ckpt)
+
+        self.swin_A, self.swin_B = stage(), stage()
+        self.cross = Cross_BasicLayer(dim=E, input_resolution=res, depth=depth, num_heads=cross_heads, window_size=ws,
+                                      mlp_ratio=mlp_ratio, use_checkpoint=use_ckpt)
+        self.to_seq_A = nn.Linear(E, d)
+        self.to_seq_B = nn.Linear(E, d)
+        head_kw = dict(kwargs)
+        head_kw.update(intermediate_vec=d, feature_map_gen='no', feature_map_size='same',
+                       sequence_length=int(res[0] * res[1] * res[2]))
+        self.crossmodal = Transformer_Net_Cross_Attention(**head_kw)
+        for bly in (self.swin_A, self.swin_B):
+            bly._init_respostnorm()
+
+    def forward(self, A, B):
+        x = self.swin_A(self.patch_embed_A(A.unsqueeze(1)))
+        y = self.swin_B(self.patch_embed_B(B.unsqueeze(1)))
+        x, y = self.cross(x, y, self.patches_resolution)
+        return self.crossmodal(self.to_seq_A(x), self.to_seq_B(y))

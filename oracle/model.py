@@ -6,7 +6,8 @@ HIP product.  Dimension-generic: token grids are 2D (H, W) or 3D (D, H, W).
 
   swin_v2_logits      SwinTransformerV2.forward  (model.py:1100-1120)
   swinfusion_logits   SwinFusion.forward         (model.py:1396-1538)
-  crossmodal_logits   Transformer_Net_Cross_Attention.forward (model.py:448-552), default options
+  crossmodal_head     Transformer_Net_Cross_Attention.forward (model.py:489-537), feature_map_size 'same'
+  swin_crossmodal_logits  the build-defined C4 composite from the pieces above
 """
 import math
 
@@ -212,6 +213,94 @@ def swinfusion_trunk(p, A, Bv, cfg):
     z = _conv(p, "conv_last1", z, 0.2)
     z = _conv(p, "conv_last2", z, 0.2)
     return _conv(p, "conv_last3", z, 1.0)[..., 0]
+
+
+# ------------------------------------------------------------------------------------------
+# crossmodal transformer (crossmodal_transformer.py, multihead_attention.py) and the C4 composite
+# ------------------------------------------------------------------------------------------
+def mha(p, pre, q_in, k_in, v_in, heads, diag):
+    """MultiheadAttention.forward without weights (multihead_attention.py:51-134): in_proj rows
+    [0,E) / [E,2E) / [2E,3E) for q / k / v, scaled-dot core, out_proj."""
+    E = q_in.shape[-1]
+    W, b = p[pre + "in_proj_weight"], p[pre + "in_proj_bias"]
+    q = F.linear(q_in, W[:E], b[:E])
+    k = F.linear(k_in, W[E:2 * E], b[E:2 * E])
+    v = F.linear(v_in, W[2 * E:], b[2 * E:])
+    out, _ = O.mha_core(q, k, v, heads, diag)
+    return F.linear(out, p[pre + "out_proj.weight"], p[pre + "out_proj.bias"])
+
+
+def _embed_tokens(x_in):
+    """sqrt(E) x + sinusoidal positions of x_in[..., 0] != 0 (crossmodal_transformer.py:72-77,
+    position_embedding.py:30-79); x_in (T, B, E)."""
+    T, B, E = x_in.shape
+    pos = O.sinusoidal_positions(x_in.transpose(0, 1)[:, :, 0])          # (B, T)
+    table = O.sinusoidal_table(T + 1, E).to(x_in.dtype)
+    return math.sqrt(E) * x_in + table[pos].transpose(0, 1)
+
+
+def encoder(p, pre, x_in, xk_in=None, xv_in=None, layers=12, heads=12, attn_mask=True):
+    """TransformerEncoder.forward (crossmodal_transformer.py:49-90, 133-165): pre-norm layers,
+    the same layer_norms.0 on query / key / value, causal mask diag 1 + |Tk - Tq|, final LN."""
+    x = _embed_tokens(x_in)
+    cross = xk_in is not None
+    if cross:
+        xk, xv = _embed_tokens(xk_in), _embed_tokens(xv_in)
+    for i in range(layers):
+        lp = f"{pre}layers.{i}."
+        ln0 = lambda t: _ln(p, lp + "layer_norms.0", t)  # noqa: E731
+        Tq = x.shape[0]
+        Tk = xk.shape[0] if cross else Tq
+        diag = O.causal_diag(Tq, Tk) if attn_mask else 0
+        xn = ln0(x)
+        a = mha(p, lp + "self_attn.", xn, ln0(xk) if cross else xn, ln0(xv) if cross else xn, heads, diag)
+        x = x + a
+        h = F.relu(_lin(p, lp + "fc1", _ln(p, lp + "layer_norms.1", x)))
+        x = x + _lin(p, lp + "fc2", h)
+    return _ln(p, pre + "layer_norm", x)
+
+
+def crossmodal_head(p, pre, x_l, x_u, layers, heads, feature_map_gen="no", attn_mask=True):
+    """Transformer_Net_Cross_Attention.forward (model.py:489-537), feature_map_size 'same',
+    mixing 'U2L_and_L2U', concat: x_l, x_u (B, T, F) -> (out_cls (B, F), logits (B, 1))."""
+    if feature_map_gen == "convolution_ul+l":
+        w = p[pre + "proj_l.weight"][:, :, 0]                           # Conv1d(T, T, 1) over the time axis
+        pl = torch.einsum("st,btf->bsf", w, x_l)
+        pu = torch.einsum("st,btf->bsf", w, x_u)
+    else:
+        pl, pu = x_l, x_u
+    pl, pu = pl.permute(1, 0, 2), pu.permute(1, 0, 2)                   # (T, B, F)
+    h_l = encoder(p, pre + "trans_l_with_u.", pl, pu, pu, layers, heads, attn_mask)
+    h_u = encoder(p, pre + "trans_u_with_l.", pu, pl, pl, layers, heads, attn_mask)
+    # trans_mem is built with layers=3 -> max(nlevels, 3) (model.py:446-470)
+    h = encoder(p, pre + "trans_mem.", torch.cat([h_l, h_u], dim=2), None, None, max(layers, 3), heads, attn_mask)
+    out_cls = _lin(p, pre + "out_layer1", h[-1])
+    return out_cls, _lin(p, pre + "out_layer2", out_cls)
+
+
+def swin_crossmodal_logits(p, A, Bv, cfg):
+    """SwinCrossmodal3D (SURVEY §8d C4 composite): per modality Conv3d(k=s=patch) + LN + Swin-V2
+    stage 1, Cross_BasicLayer, Linear to d, crossmodal head.  cfg: patch, window_size, swin_heads,
+    cross_heads, depth, layers, heads."""
+    ws, P = cfg["window_size"], cfg["patch"]
+
+    def stage(img, tag):
+        B = img.shape[0]
+        t = O.conv3d_cl(img.unsqueeze(-1), p[f"patch_embed_{tag}.proj.weight"], p[f"patch_embed_{tag}.proj.bias"],
+                        (P,) * 3, 0)
+        res = tuple(t.shape[1:-1])
+        x = _ln(p, f"patch_embed_{tag}.norm", t.reshape(B, -1, t.shape[-1]))
+        for i in range(cfg["depth"]):
+            wsz, s = _window_for(res, ws, i)
+            x = v2_block(p, f"swin_{tag}.blocks.{i}", x, res, cfg["swin_heads"], wsz, s)
+        return x, res
+
+    x, res = stage(A, "A")
+    y, _ = stage(Bv, "B")
+    x, y = cross_layer(p, "cross", x, y, res, cfg["depth"], cfg["cross_heads"], ws, res)
+    _, logits = crossmodal_head(p, "crossmodal.", _lin(p, "to_seq_A", x), _lin(p, "to_seq_B", y), cfg["layers"],
+                                cfg["heads"])
+    return logits
 
 
 def params_of(module, dtype=torch.float64):

@@ -65,3 +65,21 @@ def test_oracle_model_matches_reference(golden, name):
         else:
             nrm = float(grad.pow(2).sum().sqrt())
             assert abs(nrm - np.sqrt(gsq[i])) <= 1e-3 * max(np.sqrt(gsq[i]), 1e-12) + 1e-12, n
+
+
+def test_oracle_crossmodal_head_matches_reference(golden):
+    """The oracle's crossmodal encoder stack (used for the C4 composite) against the reference's
+    Transformer_Net_Cross_Attention logits and embedding (default options: proj_l Conv1d,
+    12 layers, 12 heads, causal)."""
+    g = golden("models.npz")
+    kw = json.loads(str(g["meta"]))["crossmodal"]["kwargs"]
+    m = M.Transformer_Net_Cross_Attention(**kw)
+    recipe.fill_params(m)
+    p = OM.params_of(m)
+    xl = torch.from_numpy(recipe.randn(4200, (2, 368, 84))).double()
+    xu = torch.from_numpy(recipe.randn(4201, (2, 368, 84))).double()
+    with torch.no_grad():
+        emb, out = OM.crossmodal_head(p, "", xl, xu, kw["nlevels"], kw["num_heads_mult"], kw["feature_map_gen"],
+                                      kw["attn_mask"])
+    assert rel(out, g["crossmodal.logits"]) < 1e-5
+    assert rel(emb, g["crossmodal.emb"]) < 1e-5
