@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="volume pairs per GPU")
     ap.add_argument("--size", type=int, default=96, help="volume side (voxels)")
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-size", type=int, default=36)
     return ap.parse_args()
@@ -158,17 +160,40 @@ def main():
     else:
         kw = model_kwargs(args.size)
         model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    graph = args.graph and world == 1
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank)
     lossf = torch.nn.BCEWithLogitsLoss()
 
-    def step():
+    def eager_step():
         opt.zero_grad(set_to_none=True)
         out = model(A, B)["binary_classification"]
         loss = lossf(out, y)
         loss.backward()
         opt.step()
         return loss
+
+    step = eager_step
+    if graph:
+        # whole-step capture (torch.cuda.graphs whole-network recipe): warm up on a side stream,
+        # capture fwd + bwd + AdamW once, then each step is one hipGraphLaunch.  The HIP kernels
+        # launch on torch's current stream, so they are captured like torch's own.
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            static_loss = lossf(model(A, B)["binary_classification"], y)
+            static_loss.backward()
+            opt.step()
+
+        def step():
+            g.replay()
+            return static_loss
 
     for _ in range(args.warmup):
         step()
@@ -185,6 +210,15 @@ def main():
     elapsed = time.perf_counter() - t0
     KernelTimer.enabled = False
     elapsed = D.max_over_ranks(elapsed, env)
+    if graph:
+        # per-kernel HIP-event timings cannot be taken inside a graph replay: one eager step
+        # after the timed region supplies them (same kernels, same shapes)
+        torch.cuda.synchronize()
+        KernelTimer.reset()
+        KernelTimer.enabled = True
+        eager_step()
+        torch.cuda.synchronize()
+        KernelTimer.enabled = False
     kern = KernelTimer.summary()
     loss_v = float(loss.item())
 
@@ -192,6 +226,7 @@ def main():
         pairs = args.batch * world * args.steps
         value = pairs / elapsed
         ms = elapsed / args.steps * 1000.0
+        steps_timed = 1 if graph else args.steps   # KernelTimer covers one eager step in graph mode
         dom_name, dom = max(kern.items(), key=lambda kv: kv[1]["total_ms"]) if kern else (None, None)
         roofline = None
         if dom is not None:
@@ -199,8 +234,8 @@ def main():
             traffic, pmc_file = latest_pmc(dom_name)
             roofline = dict(kernel=dom_name, bound="mfma", achieved=round(tflops, 3), peak=FP32_PEAK_TFLOPS,
                             unit="TFLOP/s", frac=round(tflops / FP32_PEAK_TFLOPS, 4), traffic=traffic,
-                            avg_ms=round(dom["avg_ms"], 4), launches_per_step=dom["launches"] / args.steps,
-                            share_of_step=round(dom["total_ms"] / (elapsed * 1000.0), 3),
+                            avg_ms=round(dom["avg_ms"], 4), launches_per_step=dom["launches"] / steps_timed,
+                            share_of_step=round(dom["total_ms"] / steps_timed / ms, 3),
                             algorithmic_bytes=dom["bytes_per_launch"],
                             algorithmic_gbs=round(dom["bytes_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e9, 1),
                             note="fp32 compute roof (VALU = f32 MFMA rate); head_dim 2 leaves no MFMA-shaped "
@@ -218,12 +253,13 @@ def main():
                     config=(dict(workload=f"C3: SwinFusion 3D lift, {args.size}^3 sMRI+fMRI pairs",
                                  global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
                                  patch=8, window=6, tokens_per_volume=args.size ** 3,
-                                 parallelism=f"dp{world}", checkpoint=args.checkpoint) if args.config == "c3" else
+                                 parallelism=f"dp{world}", checkpoint=args.checkpoint, graph=graph)
+                            if args.config == "c3" else
                             dict(workload=f"C4: SwinCrossmodal3D composite, {args.size}^3 pairs, crossmodal head "
                                           f"12 layers x 12 heads on {(args.size // 8) ** 3}-token sequences",
                                  global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
                                  patch=8, window=6, sequence=(args.size // 8) ** 3, parallelism=f"dp{world}",
-                                 checkpoint=args.checkpoint)),
+                                 checkpoint=args.checkpoint, graph=graph)),
                     roofline=roofline, cpu_baseline=cpu, loss=round(loss_v, 5),
                     kernels={k: dict(launches=v["launches"], avg_ms=round(v["avg_ms"], 4),
                                      total_ms=round(v["total_ms"], 2)) for k, v in kern.items()},

@@ -602,7 +602,7 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
     const int chunk = packed ? (qpl == 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl == 2 ? MMNI_PK2_KS : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    int KS = qpl == 2 ? (bwd ? 4 : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
@@ -637,10 +637,10 @@ static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*
     const int C = d->C;
     packed = false;
     qpl = 1;
-    int mf = 0, mb = 0, qf = 1;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf)) {
+    int mf = 0, mb = 0, qf = 1, qb = 1;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb)) {
         maxt = bwd ? mb : mf;
-        qpl = bwd ? 1 : qf;
+        qpl = bwd ? qb : qf;
         packed = true;
         return 0;
     }
@@ -677,10 +677,16 @@ static int fill_args(const mmni_wattn_desc* d, WAArgs& a, int& HD) {
 }
 
 // Dynamic LDS above 64 KiB: raise the per-function limit once (host-side attribute, no sync).
+// Set once per kernel (a host-side attribute, no stream work: safe inside hipGraph capture).
 static int ensure_lds_attr(void* fn, size_t bytes) {
     if (bytes <= 64 * 1024) return 0;
+    static void* done[64];
+    static int ndone = 0;
+    for (int i = 0; i < ndone; ++i)
+        if (done[i] == fn) return 0;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) { set_error("hipFuncSetAttribute: %s", hipGetErrorString(e)); return (int)e; }
+    if (ndone < 64) done[ndone++] = fn;
     return 0;
 }
 
@@ -761,7 +767,9 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg);
+    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg, qpl);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);

@@ -94,6 +94,9 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK2_CHUNK
 #define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
 #endif
+#ifndef MMNI_BWD_QPL
+#define MMNI_BWD_QPL 2        // rows per lane of the packed C = 12 backward (kind 0)
+#endif
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
 #endif
@@ -106,7 +109,8 @@ constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local tabl
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
-int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f);
+int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
+                     int& qpl_b);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the

@@ -839,6 +839,282 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] * ifs / (a.tau[tid] * kLog2e));
 }
 
+// ------------------------------------------------------------------------------------
+// backward, two rows per lane
+// ------------------------------------------------------------------------------------
+// The passes of wattn_bwd_pk_kernel with every lane carrying two rows of its window (tokens r
+// and r + N/2): pass A's K/V/metadata reads serve two queries and pass B's Q/dO/lse/delta reads
+// serve two keys, so the LDS instructions per (query, key) pair drop from ~15 (A) / ~12 (B) to
+// ~11.5 / ~7.  A window takes N/2 x KS(4) lanes: 448 threads at N = 216, one block per CU (the
+// LDS holds the bias table and its 64-bit gradient), 7 waves with up to 256 VGPRs each.
+// Kind 0 (scaled dot + table bias) only; WPB = 1.
+template <int C, int MAXT>
+__global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
+    constexpr int HD = 2, NH = C / HD, NP = NH / 2;
+    constexpr int NHP = (NH + 3) & ~3;
+    constexpr int DS = NH + kDtabPad;
+    using dt_t = std::conditional_t<kDtab32, unsigned int, unsigned long long>;
+    static_assert(NH % 2 == 0, "head pairs");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int N = g.N, NPAD = a.NPAD, KS = a.KS, NHALF = N / 2;
+    float* rowb = smem;                                   // [NPAD][2C]: pass A pk k | pk v; pass B pk a2 | pk dOs
+    float* rs_s = smem + (size_t)NPAD * 2 * C;            // [NPAD][2NH]: pass B lse2 | -delta*2^S
+    int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)NPAD * 2 * NH);
+    float* tab_s = reinterpret_cast<float*>(meta_s + NPAD);
+    dt_t* dtab_s = reinterpret_cast<dt_t*>(tab_s + (size_t)g.Tsz * NHP);
+
+    const int tid = threadIdx.x;
+    const int r = tid / KS, p = tid - r * KS;
+    const bool lane_ok = r < NHALF;
+    const int rr = lane_ok ? r : 0;
+
+    for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
+        const int row = e / NHP, h = e - row * NHP;
+        tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
+    }
+    for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0;
+    const int fexp = fix_exponent(a.maxbits, HD) - a.fix_shift;
+    const float fs = exp2f((float)fexp);
+    const float ifs = exp2f((float)-fexp);
+    const int nk = NPAD / KS;
+    const f2 qscale = splat(a.scale * kLog2e);
+
+    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+        const int w = grp;
+        const bool active = lane_ok && (w < g.nwin);
+        const bool masked = group_masked(g, grp, 1, NPAD);
+        f2 aq[2][C / 2], dO[2][C / 2], lse2[2][NP], ndl[2][NP];
+        int64_t row[2] = {0, 0};
+        int code[2] = {0, 0}, rc[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (active) {
+                const TokenInfo ti = token_info(g, w, rr + u * NHALF);
+                row[u] = ti.row;
+                code[u] = ti.code;
+                rc[u] = ti.rc;
+                load_pk<C>(aq[u], a.q + ti.row * a.qs);
+                f2 orow[C / 2];
+                load_pk<C>(dO[u], a.dout + ti.row * a.os);
+                load_pk<C>(orow, a.o + ti.row * a.os);
+#pragma unroll
+                for (int P = 0; P < NP; ++P) {
+                    aq[u][2 * P] *= qscale;
+                    aq[u][2 * P + 1] *= qscale;
+                    const f2 dd = pfma(orow[2 * P], dO[u][2 * P], orow[2 * P + 1] * dO[u][2 * P + 1]);
+                    ndl[u][P] = dd * splat(-fs);
+                    dO[u][2 * P] *= splat(fs);
+                    dO[u][2 * P + 1] *= splat(fs);
+                    lse2[u][P] = (f2){a.lse[ti.row * NH + 2 * P], a.lse[ti.row * NH + 2 * P + 1]} * kLog2e;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) { aq[u][i] = splat(0.f); dO[u][i] = splat(0.f); }
+#pragma unroll
+                for (int P = 0; P < NP; ++P) { lse2[u][P] = splat(INFINITY); ndl[u][P] = splat(0.f); }
+            }
+        }
+        // ---- stage K/V + metadata (owners write their two rows; pad rows get neutral values)
+        if (active && p == 0) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = rr + u * NHALF;
+                f2 kp[C / 2], vp[C / 2];
+                load_pk<C>(kp, a.k + row[u] * a.ks);
+                load_pk<C>(vp, a.v + row[u] * a.vs);
+                store_pk<C>(rowb + (size_t)t * 2 * C, kp);
+                store_pk<C>(rowb + (size_t)t * 2 * C + C, vp);
+                meta_s[t] = make_int2(code[u] | (rc[u] << 16), 0);
+            }
+        }
+        if (masked) {
+            for (int e = tid; e < NPAD; e += blockDim.x) {
+                if (e >= N || w >= g.nwin) {
+                    float4* z = reinterpret_cast<float4*>(rowb + (size_t)e * 2 * C);
+#pragma unroll
+                    for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    meta_s[e] = make_int2(0x7fff0000, __float_as_int(-INFINITY));
+                }
+            }
+        }
+        __syncthreads();
+
+        // ================= pass A: queries rr, rr + N/2 -> dq, dtable
+        {
+            f2 dqa[2][C / 2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) dqa[u][i] = splat(0.f);
+            const int cq0 = code[0] + g.off, cq1 = code[1] + g.off;
+            const int jb = p * nk;
+            for (int n = 0; n < nk; ++n) {
+                const int j = jb + n;
+                const int2 mm = meta_s[j];
+                const int cj = mm.x & 0xffff, rj = mm.x >> 16;
+                f2 kj[C / 2], vj[C / 2];
+                lds_row<C>(kj, rowb + (size_t)j * 2 * C);
+                lds_row<C>(vj, rowb + (size_t)j * 2 * C + C);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int tix = (u ? cq1 : cq0) - cj;
+                    f2 tb[NP];
+                    lds_tab<NP, NHP>(tb, tab_s, tix);
+                    f2 base[NP];
+                    if (masked) {
+                        const float madd = (rj == rc[u] ? 0.f : kMask2) + __int_as_float(mm.y);
+#pragma unroll
+                        for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - lse2[u][P]);
+                    } else {
+#pragma unroll
+                        for (int P = 0; P < NP; ++P) base[P] = tb[P] - lse2[u][P];
+                    }
+                    dt_t* dtp = dtab_s + tix * DS;
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) {
+                        f2 sc = pfma(aq[u][2 * P], kj[2 * P], base[P]);
+                        sc = pfma(aq[u][2 * P + 1], kj[2 * P + 1], sc);
+                        const f2 pr = exp2_2(sc);
+                        f2 tt = pfma(dO[u][2 * P], vj[2 * P], ndl[u][P]);
+                        tt = pfma(dO[u][2 * P + 1], vj[2 * P + 1], tt);
+                        const f2 dsv = pr * tt;
+                        dqa[u][2 * P] = pfma(dsv, kj[2 * P], dqa[u][2 * P]);
+                        dqa[u][2 * P + 1] = pfma(dsv, kj[2 * P + 1], dqa[u][2 * P + 1]);
+                        if (!(MMNI_ABL & 1)) {
+                            atomicAdd(&dtp[2 * P], (dt_t)fix_round(dsv.x));
+                            atomicAdd(&dtp[2 * P + 1], (dt_t)fix_round(dsv.y));
+                        }
+                    }
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) dqa[u][i] += shfl2(dqa[u][i], o);
+            }
+            if (active && p == 0) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) store_nat<C>(a.dq + row[u] * a.qs, dqa[u], a.scale * ifs);
+            }
+        }
+        __syncthreads();
+        // ---- restage: pk a2 / pk dOs and lse2 / -delta*2^S rows for pass B
+        if (active && p == 0) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = rr + u * NHALF;
+                store_pk<C>(rowb + (size_t)t * 2 * C, aq[u]);
+                store_pk<C>(rowb + (size_t)t * 2 * C + C, dO[u]);
+                f2* rs = reinterpret_cast<f2*>(rs_s + (size_t)t * 2 * NH);
+#pragma unroll
+                for (int P = 0; P < NP; ++P) { rs[P] = lse2[u][P]; rs[NP + P] = ndl[u][P]; }
+            }
+        }
+        if (masked) {
+            for (int e = tid; e < NPAD; e += blockDim.x) {
+                if (e >= N || w >= g.nwin) {
+                    float4* z = reinterpret_cast<float4*>(rowb + (size_t)e * 2 * C);
+#pragma unroll
+                    for (int c = 0; c < C / 2; ++c) z[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    f2* rs = reinterpret_cast<f2*>(rs_s + (size_t)e * 2 * NH);
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) { rs[P] = splat(INFINITY); rs[NP + P] = splat(0.f); }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ================= pass B: keys rr, rr + N/2 -> dk, dv
+        {
+            f2 kr[2][C / 2], vr[2][C / 2], dka[2][C / 2], dva[2][C / 2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (active) {
+                    load_pk<C>(kr[u], a.k + row[u] * a.ks);
+                    load_pk<C>(vr[u], a.v + row[u] * a.vs);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) { kr[u][i] = splat(0.f); vr[u][i] = splat(0.f); }
+                }
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) { dka[u][i] = splat(0.f); dva[u][i] = splat(0.f); }
+            }
+            const int ck0 = g.off - code[0], ck1 = g.off - code[1];
+            const int ib = p * nk;
+            for (int n = 0; n < nk; ++n) {
+                const int i = ib + n;
+                const int2 mm = meta_s[i];
+                const int ci = mm.x & 0xffff, ri = mm.x >> 16;
+                f2 ai[C / 2], gi[C / 2];
+                lds_row<C>(ai, rowb + (size_t)i * 2 * C);
+                lds_row<C>(gi, rowb + (size_t)i * 2 * C + C);
+                f2 rsi[2 * NP];
+                {
+                    const float4* rq = reinterpret_cast<const float4*>(rs_s + (size_t)i * 2 * NH);
+#pragma unroll
+                    for (int c = 0; c < NP; ++c) {
+                        const float4 x = rq[c];
+                        rsi[2 * c] = (f2){x.x, x.y};
+                        rsi[2 * c + 1] = (f2){x.z, x.w};
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int tix = ci + (u ? ck1 : ck0);
+                    f2 tb[NP];
+                    lds_tab<NP, NHP>(tb, tab_s, tix);
+                    f2 base[NP];
+                    if (masked) {
+                        const float madd = (ri == rc[u] ? 0.f : kMask2) + __int_as_float(mm.y);
+#pragma unroll
+                        for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - rsi[P]);
+                    } else {
+#pragma unroll
+                        for (int P = 0; P < NP; ++P) base[P] = tb[P] - rsi[P];
+                    }
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) {
+                        f2 sc = pfma(ai[2 * P], kr[u][2 * P], base[P]);
+                        sc = pfma(ai[2 * P + 1], kr[u][2 * P + 1], sc);
+                        const f2 pr = exp2_2(sc);
+                        f2 tt = pfma(gi[2 * P], vr[u][2 * P], rsi[NP + P]);
+                        tt = pfma(gi[2 * P + 1], vr[u][2 * P + 1], tt);
+                        const f2 dsv = pr * tt;
+                        dva[u][2 * P] = pfma(pr, gi[2 * P], dva[u][2 * P]);
+                        dva[u][2 * P + 1] = pfma(pr, gi[2 * P + 1], dva[u][2 * P + 1]);
+                        dka[u][2 * P] = pfma(dsv, ai[2 * P], dka[u][2 * P]);
+                        dka[u][2 * P + 1] = pfma(dsv, ai[2 * P + 1], dka[u][2 * P + 1]);
+                    }
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) {
+                        dka[u][i] += shfl2(dka[u][i], o);
+                        dva[u][i] += shfl2(dva[u][i], o);
+                    }
+            }
+            if (active && p == 0) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    store_nat<C>(a.dv + row[u] * a.vs, dva[u], ifs);
+                    store_nat<C>(a.dk + row[u] * a.ks, dka[u], kLn2 * ifs);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
+        const dt_t v = dtab_s[(e / NH) * DS + e % NH];
+        if (v != 0) atomicAdd(&a.dtab_fix[e], kDtab32 ? (unsigned long long)(long long)(int)v : (unsigned long long)v);
+    }
+}
+
 template <int C, int MAXT>
 static void* pk_fwd(int kind) {
     return kind ? reinterpret_cast<void*>(&wattn_fwd_pk_kernel<C, 1, MAXT>)
@@ -859,13 +1135,26 @@ static void* pk2_fwd(int kind) {
 // Forward blocks of <= 512 threads (KS = 2 at N = 216): two blocks share a CU, so one block's
 // K/V gather overlaps the other's compute.  The backward's LDS (bias table + its 64-bit
 // gradient) allows one block per CU; it keeps 1024 threads (KS = 4) for occupancy.
-// qpl_f: queries per lane of the forward (2: wattn_fwd_pk2_kernel, windows of even N).
-int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f) {
+// qpl_f / qpl_b: rows per lane of the forward / backward (2: the pk2 kernels, windows of even N;
+// the two-row backward needs one window per block, N > 128).
+int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
+                     int& qpl_b) {
     const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
+    const bool two_b = MMNI_BWD_QPL == 2 && kind == 0 && N % 2 == 0 && N > 128;
     qpl_f = two ? 2 : 1;
+    qpl_b = 1;
     if (C == 12) {
         kf = two ? pk2_fwd<12, 512>(kind) : pk_fwd<12, 512>(kind);
-        kb = pk_bwd<12, 1024>(kind); maxt_f = 512; maxt_b = 1024; return 1;
+        maxt_f = 512;
+        if (two_b) {
+            kb = reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<12, 512>);
+            maxt_b = 512;
+            qpl_b = 2;
+        } else {
+            kb = pk_bwd<12, 1024>(kind);
+            maxt_b = 1024;
+        }
+        return 1;
     }
     if (C == 24) { kf = pk_fwd<24, 512>(kind); kb = pk_bwd<24, 512>(kind); maxt_f = 512; maxt_b = 512; qpl_f = 1; return 1; }
     return 0;

