@@ -61,7 +61,18 @@ __global__ __launch_bounds__(1024) void wattn_absmax_dout4_kernel(const float4* 
                                                                   const unsigned int* vmax, unsigned int* maxbits) {
     __shared__ float red[16];
     float md = 0.f;
-    for (long long i = blockIdx.x * 1024ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 1024) {
+    // four independent 16-B loads in flight per lane (one per lane leaves HBM latency exposed)
+    const long long stride = (long long)gridDim.x * 1024;
+    long long i = blockIdx.x * 1024ll + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        float4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = dout[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            md = fmaxf(md, fmaxf(fmaxf(fabsf(x[u].x), fabsf(x[u].y)), fmaxf(fabsf(x[u].z), fabsf(x[u].w))));
+    }
+    for (; i < n4; i += stride) {
         const float4 x = dout[i];
         md = fmaxf(md, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     }
@@ -770,7 +781,7 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg, qpl);
     if (rc) return rc;
     MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");
-    if (rc) return rc;
+    MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / 2) * cfg.KS, "wattn_bwd: two-row kernel launch shape");
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;

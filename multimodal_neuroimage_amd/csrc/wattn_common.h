@@ -100,6 +100,12 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
 #endif
+#ifndef MMNI_PK2_PAIRK
+#define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
+#endif
+#ifndef MMNI_PK2_KVLDS
+#define MMNI_PK2_KVLDS 1      // two-row backward: pass B's K/V rows read from the pass A staging
+#endif
 #ifndef MMNI_DTAB32
 #define MMNI_DTAB32 0
 #endif

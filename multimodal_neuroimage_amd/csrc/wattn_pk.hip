@@ -887,17 +887,40 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
         f2 aq[2][C / 2], dO[2][C / 2], lse2[2][NP], ndl[2][NP];
         int64_t row[2] = {0, 0};
         int code[2] = {0, 0}, rc[2] = {0, 0};
+        if (active) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (active) {
+            for (int u = 0; u < 2; ++u) {
                 const TokenInfo ti = token_info(g, w, rr + u * NHALF);
                 row[u] = ti.row;
                 code[u] = ti.code;
                 rc[u] = ti.rc;
-                load_pk<C>(aq[u], a.q + ti.row * a.qs);
+            }
+        }
+        // K/V staging split over the row pair's KS = 4 lanes: lane p moves float4 chunks p, p + 4,
+        // p + 8 of [K row 0 | V row 0 | K row 1 | V row 1] (3 chunks each), loaded in the same
+        // round as the Q/dO/O rows below.  A chunk keeps its offset in the pk row layout, with its
+        // components reordered (x, z, y, w) as store_pk does.
+        constexpr int KVCH = 4 * (C / 4);       // float4 chunks of the two K and V rows
+        constexpr int KVPL = (KVCH + 3) / 4;    // per lane
+        float4 kvc[KVPL];
+        if (active) {
+#pragma unroll
+            for (int m = 0; m < KVPL; ++m) {
+                const int c = p + 4 * m, u = c / (2 * (C / 4)), cc = c - u * 2 * (C / 4);
+                const bool isv = cc >= C / 4;
+                const float* src = isv ? a.v + row[u] * a.vs : a.k + row[u] * a.ks;
+                kvc[m] = c < KVCH ? *reinterpret_cast<const float4*>(src + 4 * (cc - (isv ? C / 4 : 0)))
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (active) {
+                const int64_t rw = row[u];
+                load_pk<C>(aq[u], a.q + rw * a.qs);
                 f2 orow[C / 2];
-                load_pk<C>(dO[u], a.dout + ti.row * a.os);
-                load_pk<C>(orow, a.o + ti.row * a.os);
+                load_pk<C>(dO[u], a.dout + rw * a.os);
+                load_pk<C>(orow, a.o + rw * a.os);
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
                     aq[u][2 * P] *= qscale;
@@ -906,7 +929,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
                     ndl[u][P] = dd * splat(-fs);
                     dO[u][2 * P] *= splat(fs);
                     dO[u][2 * P + 1] *= splat(fs);
-                    lse2[u][P] = (f2){a.lse[ti.row * NH + 2 * P], a.lse[ti.row * NH + 2 * P + 1]} * kLog2e;
+                    lse2[u][P] = (f2){a.lse[rw * NH + 2 * P], a.lse[rw * NH + 2 * P + 1]} * kLog2e;
                 }
             } else {
 #pragma unroll
@@ -915,17 +938,20 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
                 for (int P = 0; P < NP; ++P) { lse2[u][P] = splat(INFINITY); ndl[u][P] = splat(0.f); }
             }
         }
-        // ---- stage K/V + metadata (owners write their two rows; pad rows get neutral values)
-        if (active && p == 0) {
+        // ---- stage K/V + metadata (pad rows get neutral values)
+        if (active) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int t = rr + u * NHALF;
-                f2 kp[C / 2], vp[C / 2];
-                load_pk<C>(kp, a.k + row[u] * a.ks);
-                load_pk<C>(vp, a.v + row[u] * a.vs);
-                store_pk<C>(rowb + (size_t)t * 2 * C, kp);
-                store_pk<C>(rowb + (size_t)t * 2 * C + C, vp);
-                meta_s[t] = make_int2(code[u] | (rc[u] << 16), 0);
+            for (int m = 0; m < KVPL; ++m) {
+                const int c = p + 4 * m, u = c / (2 * (C / 4)), cc = c - u * 2 * (C / 4);
+                if (c < KVCH) {
+                    const float4 t = kvc[m];
+                    *reinterpret_cast<float4*>(rowb + (size_t)(rr + u * NHALF) * 2 * C + 4 * cc) =
+                        make_float4(t.x, t.z, t.y, t.w);
+                }
+            }
+            if (p == 0) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) meta_s[rr + u * NHALF] = make_int2(code[u] | (rc[u] << 16), 0);
             }
         }
         if (masked) {
@@ -940,6 +966,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
         }
         __syncthreads();
 
+        f2 kr[2][C / 2], vr[2][C / 2];   // pass B's own K/V rows, read from the pass A staging
         // ================= pass A: queries rr, rr + N/2 -> dq, dtable
         {
             f2 dqa[2][C / 2];
@@ -948,43 +975,87 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) dqa[u][i] = splat(0.f);
             const int cq0 = code[0] + g.off, cq1 = code[1] + g.off;
-            const int jb = p * nk;
-            for (int n = 0; n < nk; ++n) {
-                const int j = jb + n;
-                const int2 mm = meta_s[j];
-                const int cj = mm.x & 0xffff, rj = mm.x >> 16;
-                f2 kj[C / 2], vj[C / 2];
-                lds_row<C>(kj, rowb + (size_t)j * 2 * C);
-                lds_row<C>(vj, rowb + (size_t)j * 2 * C + C);
+            // one (query u, key) pair: probability, dS (scaled by 2^S) and the dq update
+            auto pair = [&](int u, const f2 (&tb)[NP], const f2 (&kj)[C / 2], const f2 (&vj)[C / 2], int2 mk,
+                            f2 (&dsv)[NP]) {
+                f2 base[NP];
+                if (masked) {
+                    const float madd = ((mk.x >> 16) == rc[u] ? 0.f : kMask2) + __int_as_float(mk.y);
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int tix = (u ? cq1 : cq0) - cj;
-                    f2 tb[NP];
-                    lds_tab<NP, NHP>(tb, tab_s, tix);
-                    f2 base[NP];
-                    if (masked) {
-                        const float madd = (rj == rc[u] ? 0.f : kMask2) + __int_as_float(mm.y);
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - lse2[u][P]);
+                } else {
 #pragma unroll
-                        for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - lse2[u][P]);
-                    } else {
+                    for (int P = 0; P < NP; ++P) base[P] = tb[P] - lse2[u][P];
+                }
 #pragma unroll
-                        for (int P = 0; P < NP; ++P) base[P] = tb[P] - lse2[u][P];
-                    }
-                    dt_t* dtp = dtab_s + tix * DS;
+                for (int P = 0; P < NP; ++P) {
+                    f2 sc = pfma(aq[u][2 * P], kj[2 * P], base[P]);
+                    sc = pfma(aq[u][2 * P + 1], kj[2 * P + 1], sc);
+                    const f2 pr = exp2_2(sc);
+                    f2 tt = pfma(dO[u][2 * P], vj[2 * P], ndl[u][P]);
+                    tt = pfma(dO[u][2 * P + 1], vj[2 * P + 1], tt);
+                    dsv[P] = pr * tt;
+                    dqa[u][2 * P] = pfma(dsv[P], kj[2 * P], dqa[u][2 * P]);
+                    dqa[u][2 * P + 1] = pfma(dsv[P], kj[2 * P + 1], dqa[u][2 * P + 1]);
+                }
+            };
+            auto scatter = [&](int tix, const f2 (&dsv)[NP]) {
+                if (MMNI_ABL & 1) return;
+                dt_t* dtp = dtab_s + tix * DS;
 #pragma unroll
-                    for (int P = 0; P < NP; ++P) {
-                        f2 sc = pfma(aq[u][2 * P], kj[2 * P], base[P]);
-                        sc = pfma(aq[u][2 * P + 1], kj[2 * P + 1], sc);
-                        const f2 pr = exp2_2(sc);
-                        f2 tt = pfma(dO[u][2 * P], vj[2 * P], ndl[u][P]);
-                        tt = pfma(dO[u][2 * P + 1], vj[2 * P + 1], tt);
-                        const f2 dsv = pr * tt;
-                        dqa[u][2 * P] = pfma(dsv, kj[2 * P], dqa[u][2 * P]);
-                        dqa[u][2 * P + 1] = pfma(dsv, kj[2 * P + 1], dqa[u][2 * P + 1]);
-                        if (!(MMNI_ABL & 1)) {
-                            atomicAdd(&dtp[2 * P], (dt_t)fix_round(dsv.x));
-                            atomicAdd(&dtp[2 * P + 1], (dt_t)fix_round(dsv.y));
-                        }
+                for (int P = 0; P < NP; ++P) {
+                    atomicAdd(&dtp[2 * P], (dt_t)fix_round(dsv[P].x));
+                    atomicAdd(&dtp[2 * P + 1], (dt_t)fix_round(dsv[P].y));
+                }
+            };
+            // Paired keys: when the window's second half is a whole number of planes later than
+            // its first (N/2 a multiple of wh*ww: code(t + N/2) = code(t) + const), query rr + N/2
+            // and key j + N/2 have the same relative offset as query rr and key j.  The lane takes
+            // keys j and j + N/2 together: 4 pairs on 3 table rows, the shared row's two dS summed
+            // before one set of atomics (|sum| < 2^31, see fix_exponent): 18 atomics and 3 table
+            // reads per 4 pairs instead of 24 and 4.
+            const bool paired = MMNI_PK2_PAIRK && NPAD == N && NHALF % (g.wh * g.ww) == 0 && NHALF % KS == 0;
+            if (paired) {
+                const int nk2 = NHALF / KS, jb = p * nk2;
+                for (int n = 0; n < ((MMNI_ABL & 4) ? 0 : nk2); ++n) {
+                    const int j0 = jb + n, j1 = j0 + NHALF;
+                    const int2 m0 = meta_s[j0], m1 = meta_s[j1];
+                    const int tA = cq0 - (m0.x & 0xffff);   // (rr, j0) and (rr + N/2, j1)
+                    const int tC = cq1 - (m0.x & 0xffff);   // (rr + N/2, j0)
+                    const int tB = cq0 - (m1.x & 0xffff);   // (rr, j1)
+                    f2 kj[C / 2], vj[C / 2], tbA[NP], tb2[NP], dsA[NP], ds[NP];
+                    lds_row<C>(kj, rowb + (size_t)j0 * 2 * C);
+                    lds_row<C>(vj, rowb + (size_t)j0 * 2 * C + C);
+                    lds_tab<NP, NHP>(tbA, tab_s, tA);
+                    lds_tab<NP, NHP>(tb2, tab_s, tC);
+                    pair(0, tbA, kj, vj, m0, dsA);
+                    pair(1, tb2, kj, vj, m0, ds);
+                    scatter(tC, ds);
+                    __builtin_amdgcn_sched_barrier(0);   // keep key j1's reads behind key j0's work
+                    lds_row<C>(kj, rowb + (size_t)j1 * 2 * C);
+                    lds_row<C>(vj, rowb + (size_t)j1 * 2 * C + C);
+                    lds_tab<NP, NHP>(tb2, tab_s, tB);
+                    pair(0, tb2, kj, vj, m1, ds);
+                    scatter(tB, ds);
+                    pair(1, tbA, kj, vj, m1, ds);
+#pragma unroll
+                    for (int P = 0; P < NP; ++P) ds[P] += dsA[P];
+                    scatter(tA, ds);
+                }
+            } else {
+                const int jb = p * nk;
+                for (int n = 0; n < ((MMNI_ABL & 4) ? 0 : nk); ++n) {
+                    const int j = jb + n;
+                    const int2 mk = meta_s[j];
+                    f2 kj[C / 2], vj[C / 2], tb[NP], ds[NP];
+                    lds_row<C>(kj, rowb + (size_t)j * 2 * C);
+                    lds_row<C>(vj, rowb + (size_t)j * 2 * C + C);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int tix = (u ? cq1 : cq0) - (mk.x & 0xffff);
+                        lds_tab<NP, NHP>(tb, tab_s, tix);
+                        pair(u, tb, kj, vj, mk, ds);
+                        scatter(tix, ds);
                     }
                 }
             }
@@ -997,6 +1068,19 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
             if (active && p == 0) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u) store_nat<C>(a.dq + row[u] * a.qs, dqa[u], a.scale * ifs);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (active && MMNI_PK2_KVLDS) {
+                    lds_row<C>(kr[u], rowb + (size_t)(rr + u * NHALF) * 2 * C);
+                    lds_row<C>(vr[u], rowb + (size_t)(rr + u * NHALF) * 2 * C + C);
+                } else if (active) {
+                    load_pk<C>(kr[u], a.k + row[u] * a.ks);
+                    load_pk<C>(vr[u], a.v + row[u] * a.vs);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) { kr[u][i] = splat(0.f); vr[u][i] = splat(0.f); }
+                }
             }
         }
         __syncthreads();
@@ -1028,25 +1112,17 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
 
         // ================= pass B: keys rr, rr + N/2 -> dk, dv
         {
-            f2 kr[2][C / 2], vr[2][C / 2], dka[2][C / 2], dva[2][C / 2];
+            f2 dka[2][C / 2], dva[2][C / 2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (active) {
-                    load_pk<C>(kr[u], a.k + row[u] * a.ks);
-                    load_pk<C>(vr[u], a.v + row[u] * a.vs);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < C / 2; ++i) { kr[u][i] = splat(0.f); vr[u][i] = splat(0.f); }
-                }
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) { dka[u][i] = splat(0.f); dva[u][i] = splat(0.f); }
-            }
             const int ck0 = g.off - code[0], ck1 = g.off - code[1];
             const int ib = p * nk;
-            for (int n = 0; n < nk; ++n) {
+            for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nk); ++n) {
                 const int i = ib + n;
-                const int2 mm = meta_s[i];
-                const int ci = mm.x & 0xffff, ri = mm.x >> 16;
+                const int2 mcur = meta_s[i];
+                const int ci = mcur.x & 0xffff, ri = mcur.x >> 16;
                 f2 ai[C / 2], gi[C / 2];
                 lds_row<C>(ai, rowb + (size_t)i * 2 * C);
                 lds_row<C>(gi, rowb + (size_t)i * 2 * C + C);
@@ -1067,7 +1143,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
                     lds_tab<NP, NHP>(tb, tab_s, tix);
                     f2 base[NP];
                     if (masked) {
-                        const float madd = (ri == rc[u] ? 0.f : kMask2) + __int_as_float(mm.y);
+                        const float madd = (ri == rc[u] ? 0.f : kMask2) + __int_as_float(mcur.y);
 #pragma unroll
                         for (int P = 0; P < NP; ++P) base[P] = tb[P] + (splat(madd) - rsi[P]);
                     } else {
