@@ -26,6 +26,9 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk2?_kernel<(\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
+    m = re.search(r"mmni::wattn_bwd_pk2_kernel<(\d+), \d+>", name)   # kind 0 only
+    if m:
+        return f"wattn_bwd_k0_C{m.group(1)}"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
     if m:
         return f"{m.group(1)}_hd{m.group(2)}"
