@@ -17,6 +17,25 @@ namespace blk {
 
 using namespace tt;
 
+#ifndef MMNI_LLF_U
+#define MMNI_LLF_U 4
+#endif
+#ifndef MMNI_LLB_U
+#define MMNI_LLB_U 2
+#endif
+constexpr int kLlfU = MMNI_LLF_U;   // tiles per step, ln_linear_fwd
+constexpr int kLlbU = MMNI_LLB_U;   // tiles per step, ln_linear_bwd (N = 12, 24)
+// N = 36 keeps one tile per step: two would take it to 2 waves / SIMD (measured 270 vs 257 us)
+constexpr int llb_u(int n) { return n == 36 ? 1 : kLlbU; }
+#ifndef MMNI_LLF_LDS
+#define MMNI_LLF_LDS 1
+#endif
+constexpr bool kLlfLds = MMNI_LLF_LDS;   // ln_linear_fwd N > 12: outputs staged through LDS
+#ifndef MMNI_LLB_LDS
+#define MMNI_LLB_LDS 1
+#endif
+constexpr bool kLlbLds = MMNI_LLB_LDS;   // ln_linear_bwd N > 12: dy tiles staged through LDS
+
 struct TokArgs {
     int64_t rows;
     float eps;
@@ -38,7 +57,7 @@ struct TokArgs {
 // ------------------------------------------------------------------------------------
 // y = LN(x) W^T + b, per 16-token tile: LN on the feature-major operand, NT MFMA output tiles
 // ------------------------------------------------------------------------------------
-template <int N>
+template <int N, int U>
 __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
     constexpr int NT = (N + 15) / 16;
     const int lane = threadIdx.x & 63;
@@ -61,27 +80,53 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
     }
 #pragma unroll
     for (int s = 0; s < CS; ++s) { gm[s] = a.gamma[4 * s + g]; bt[s] = a.beta[4 * s + g]; }
+    __shared__ __attribute__((aligned(16))) float ys_all[kLlfLds && N > 12 ? 4 * 16 * N : 4];
+    float* ys = ys_all + (kLlfLds && N > 12 ? (threadIdx.x >> 6) * 16 * N : 0);
     const int64_t tiles = (a.rows + 15) / 16;
-    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
-        const int64_t t0 = tile * 16;
-        float v[CS];
-        tl.load_fm<CS, C>(a.x, t0, v);
-        float mean, rstd;
-        ln_stats(v, a.eps, mean, rstd);
-        float xn[CS];
+    // U consecutive tiles per step: their loads are issued together (one tile's 768 B per wave
+    // in flight leaves the HBM latency exposed at this register budget)
+    for (int64_t tb = wave * U; tb < tiles; tb += nwaves * U) {
+        float v[U][CS];
 #pragma unroll
-        for (int s = 0; s < CS; ++s) xn[s] = fmaf((v[s] - mean) * rstd, gm[s], bt[s]);
-        const bool ok = tl.token_ok(t0);
+        for (int u = 0; u < U; ++u) tl.load_fm<CS, C>(a.x, (tb + u) * 16, v[u]);   // rows past the end load 0
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            f4 acc = bc[nt];
+        for (int u = 0; u < U; ++u) {
+            const int64_t t0 = (tb + u) * 16;
+            float mean, rstd;
+            ln_stats(v[u], a.eps, mean, rstd);
+            float xn[CS];
 #pragma unroll
-            for (int s = 0; s < CS; ++s) acc = mfma(wa[nt][s], xn[s], acc);
-            if (ok && nt * 16 + 4 * g < N) *reinterpret_cast<f4*>(a.y + (t0 + t) * N + nt * 16 + 4 * g) = acc;
-        }
-        if (ok && g == 0) {
-            a.mean[t0 + t] = mean;
-            a.rstd[t0 + t] = rstd;
+            for (int s = 0; s < CS; ++s) xn[s] = fmaf((v[u][s] - mean) * rstd, gm[s], bt[s]);
+            const bool ok = tl.token_ok(t0);
+            if constexpr (kLlfLds && N > 12) {
+                // the tile's 16 x N outputs go through the wave's LDS slab, then out as contiguous
+                // 16-B stores (the accumulator layout writes each token row in N / 16 pieces)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    f4 acc = bc[nt];
+#pragma unroll
+                    for (int s = 0; s < CS; ++s) acc = mfma(wa[nt][s], xn[s], acc);
+                    if (nt * 16 + 4 * g < N) *reinterpret_cast<f4*>(ys + t * N + nt * 16 + 4 * g) = acc;
+                }
+                const int64_t nvec = (a.rows - t0 < 16 ? a.rows - t0 : 16) * (N / 4);
+#pragma unroll
+                for (int k = 0; k < (4 * N + 63) / 64; ++k) {
+                    const int e = k * 64 + lane;
+                    if (e < nvec) *reinterpret_cast<f4*>(a.y + t0 * N + 4 * e) = *reinterpret_cast<const f4*>(ys + 4 * e);
+                }
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    f4 acc = bc[nt];
+#pragma unroll
+                    for (int s = 0; s < CS; ++s) acc = mfma(wa[nt][s], xn[s], acc);
+                    if (ok && nt * 16 + 4 * g < N) *reinterpret_cast<f4*>(a.y + (t0 + t) * N + nt * 16 + 4 * g) = acc;
+                }
+            }
+            if (ok && g == 0) {
+                a.mean[t0 + t] = mean;
+                a.rstd[t0 + t] = rstd;
+            }
         }
     }
 }
@@ -89,7 +134,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
 // ------------------------------------------------------------------------------------
 // dx = LN_bwd(dy W) + dres;  dW = dy^T LN(x),  db = colsum dy,  dgamma, dbeta
 // ------------------------------------------------------------------------------------
-template <int N>
+template <int N, int U>
 __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
     constexpr int NT = (N + 15) / 16;
     constexpr int NS = N / 4;   // k-steps over the N gradient columns
@@ -113,41 +158,89 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) { dw[nt] = zero4(); db[nt] = 0.f; }
 
+    constexpr bool kDyLds = kLlbLds && N > 12;
+    constexpr int DYV = (4 * N + 63) / 64;   // 16-B vectors per lane per dy tile
+    __shared__ __attribute__((aligned(16))) float dys_all[kDyLds ? 4 * U * 16 * N : 4];
+    float* dys = dys_all + (kDyLds ? (threadIdx.x >> 6) * U * 16 * N : 0);
     const int64_t tiles = (a.rows + 15) / 16;
-    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
-        const int64_t t0 = tile * 16;
-        // dxn^T = W^T dy^T: accumulator chunk = dL/dLN(x) of channels 4 g + i of token t0 + t
-        float dyb[NS];
-        tl.load_fm<NS, N>(a.dy, t0, dyb);
-        f4 dxn = zero4();
+    // U consecutive tiles per step, all loads first (see ln_linear_fwd_kernel)
+    for (int64_t tb = wave * U; tb < tiles; tb += nwaves * U) {
+        float dyb[U][NS], xa[U][4], mt[U][4], rt[U][4], dya[U][NT][4], mu[U], ru[U];
+        f4 xc[U];
+        if constexpr (kDyLds) {
+            // dy tiles (16 x N floats, contiguous) in with 16-B loads, both operand maps out of LDS
+            f4 dv[U][DYV];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) dxn = mfma(wt[s], dyb[s], dxn);
-        // LayerNorm backward on the chunk (+ residual gradient)
-        const bool ok = tl.chunk_ok(t0);
-        const bool tok = tl.token_ok(t0);
-        const float m = tok ? a.mean[t0 + t] : 0.f, rs = tok ? a.rstd[t0 + t] : 0.f;
-        const f4 xc = ok ? *reinterpret_cast<const f4*>(a.x + (t0 + t) * C + 4 * g) : zero4();
-        const f4 xh = ok ? (xc - m) * rs : zero4();
-        f4 dx = ln_bwd_chunk(dxn, xh, gm4, rs);
-        if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
-        if (ok) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
-        dg += dxn * xh;
-        dbt += dxn;
-        // dW = dy^T xn over the tile's tokens (token-major operands; xn recomputed)
-        float xa[4], mt[4], rt[4], xnt[4];
-        tl.load_tm<C>(a.x, t0, 0, C, xa);
-        tl.load_tm_scalar(a.mean, t0, mt);
-        tl.load_tm_scalar(a.rstd, t0, rt);
+            for (int u = 0; u < U; ++u) {
+                const int64_t t0 = (tb + u) * 16;
+                const int64_t nvec = (a.rows - t0 < 16 ? a.rows - t0 : 16) * (N / 4);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) xnt[s] = t < C ? fmaf((xa[s] - mt[s]) * rt[s], gmt, btt) : 0.f;
+                for (int k = 0; k < DYV; ++k) {
+                    const int e = k * 64 + lane;
+                    dv[u][k] = e < nvec ? *reinterpret_cast<const f4*>(a.dy + t0 * N + 4 * e) : zero4();
+                }
+            }
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            float dya[4];
-            tl.load_tm<N>(a.dy, t0, nt * 16, N - nt * 16, dya);
+            for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                dw[nt] = mfma(dya[s], xnt[s], dw[nt]);
-                db[nt] += dya[s];
+                for (int k = 0; k < DYV; ++k) {
+                    const int e = k * 64 + lane;
+                    if (e < 4 * N) *reinterpret_cast<f4*>(dys + u * 16 * N + 4 * e) = dv[u][k];
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float* ds = dys + u * 16 * N;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) dyb[u][s] = ds[t * N + 4 * s + g];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) dya[u][nt][s] = nt * 16 + t < N ? ds[(4 * s + g) * N + nt * 16 + t] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t0 = (tb + u) * 16;
+            if constexpr (!kDyLds) tl.load_fm<NS, N>(a.dy, t0, dyb[u]);
+            const bool ok = tl.chunk_ok(t0);
+            const bool tok = tl.token_ok(t0);
+            mu[u] = tok ? a.mean[t0 + t] : 0.f;
+            ru[u] = tok ? a.rstd[t0 + t] : 0.f;
+            xc[u] = ok ? *reinterpret_cast<const f4*>(a.x + (t0 + t) * C + 4 * g) : zero4();
+            tl.load_tm<C>(a.x, t0, 0, C, xa[u]);
+            tl.load_tm_scalar(a.mean, t0, mt[u]);
+            tl.load_tm_scalar(a.rstd, t0, rt[u]);
+            if constexpr (!kDyLds) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) tl.load_tm<N>(a.dy, t0, nt * 16, N - nt * 16, dya[u][nt]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t0 = (tb + u) * 16;
+            // dxn^T = W^T dy^T: accumulator chunk = dL/dLN(x) of channels 4 g + i of token t0 + t
+            f4 dxn = zero4();
+#pragma unroll
+            for (int s = 0; s < NS; ++s) dxn = mfma(wt[s], dyb[u][s], dxn);
+            // LayerNorm backward on the chunk (+ residual gradient)
+            const bool ok = tl.chunk_ok(t0);
+            const f4 xh = ok ? (xc[u] - mu[u]) * ru[u] : zero4();
+            f4 dx = ln_bwd_chunk(dxn, xh, gm4, ru[u]);
+            if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
+            if (ok) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
+            dg += dxn * xh;
+            dbt += dxn;
+            // dW = dy^T xn over the tile's tokens (token-major operands; xn recomputed)
+            float xnt[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) xnt[s] = t < C ? fmaf((xa[u][s] - mt[u][s]) * rt[u][s], gmt, btt) : 0.f;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    dw[nt] = mfma(dya[u][nt][s], xnt[s], dw[nt]);
+                    db[nt] += dya[u][nt][s];
+                }
             }
         }
     }
@@ -253,9 +346,10 @@ extern "C" int mmni_ln_linear_fwd(const mmni_tok_desc* d, const float* x, const 
     hipStream_t s = (hipStream_t)stream;
 #define MMNI_LLF(NN)                                                                                  \
     if (d->N == NN) {                                                                                 \
-        static const int waves = waves_of(&blk::ln_linear_fwd_kernel<NN>);                          \
-        const int64_t grid = (tiles + 3) / 4 < waves / 4 ? (tiles + 3) / 4 : waves / 4;             \
-        blk::ln_linear_fwd_kernel<NN><<<(int)grid, 256, 0, s>>>(a);                                  \
+        static const int waves = waves_of(&blk::ln_linear_fwd_kernel<NN, blk::kLlfU>);                   \
+        const int64_t need = (tiles + 4 * blk::kLlfU - 1) / (4 * blk::kLlfU);                                  \
+        const int64_t grid = need < waves / 4 ? need : waves / 4;                                    \
+        blk::ln_linear_fwd_kernel<NN, blk::kLlfU><<<(int)grid, 256, 0, s>>>(a);                           \
     }
     MMNI_LLF(12) MMNI_LLF(24) MMNI_LLF(36)
 #undef MMNI_LLF
@@ -287,11 +381,11 @@ extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const
     int waves = 0;
 #define MMNI_LLB(NN)                                                                                  \
     if (N == NN) {                                                                                    \
-        static const int wv = waves_of(&blk::ln_linear_bwd_kernel<NN>);                             \
+        static const int wv = waves_of(&blk::ln_linear_bwd_kernel<NN, blk::llb_u(NN)>);                      \
         waves = wv < kNumCU * 8 * 4 ? wv : kNumCU * 8 * 4;                                           \
         a.partA = reinterpret_cast<float*>(workspace);                                              \
         a.partB = a.partA + (size_t)waves * (N * C + N);                                            \
-        blk::ln_linear_bwd_kernel<NN><<<waves / 4, 256, 0, s>>>(a);                                  \
+        blk::ln_linear_bwd_kernel<NN, blk::llb_u(NN)><<<waves / 4, 256, 0, s>>>(a);                           \
     }
     MMNI_LLB(12) MMNI_LLB(24) MMNI_LLB(36)
 #undef MMNI_LLB
