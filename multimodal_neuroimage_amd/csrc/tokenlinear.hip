@@ -87,6 +87,71 @@ __global__ __launch_bounds__(256) void token_linear_kernel(TLinArgs a) {
         for (int n = threadIdx.x; n < N; n += blockDim.x) b2l[n] = a.b2 ? a.b2[n] : 0.f;
     }
     __syncthreads();
+    if constexpr (K == 12 && N == 12 && EPI == 0) {
+        if (a.ldx == K && a.ldy == N) {
+            // Contiguous rows: the block's 256 x 12 tile moves between HBM and LDS as contiguous
+            // 16-B vectors (a lane's own 48-B row, read and written directly, leaves every
+            // instruction touching a third of each line: the measured write traffic doubled).
+            // The residual is added on the way out.
+            __shared__ __attribute__((aligned(16))) float tile[256 * 12];
+            float4* t4 = reinterpret_cast<float4*>(tile);
+            const float4* x4 = reinterpret_cast<const float4*>(a.x);
+            const float4* r4 = reinterpret_cast<const float4*>(a.res);
+            float4* y4 = reinterpret_cast<float4*>(a.y);
+            for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < a.rows; r0 += (int64_t)gridDim.x * 256) {
+                const int nr = a.rows - r0 < 256 ? (int)(a.rows - r0) : 256;
+                const int nv = nr * 3;
+                float4 xin[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int e = k * 256 + threadIdx.x;
+                    if (e < nv) xin[k] = x4[r0 * 3 + e];
+                }
+                __syncthreads();   // the previous tile's stores have read the LDS tile
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int e = k * 256 + threadIdx.x;
+                    if (e < nv) t4[e] = xin[k];
+                }
+                __syncthreads();
+                if ((int)threadIdx.x < nr) {
+                    float xr[12];
+                    ld_row<12>(xr, tile + threadIdx.x * 12);
+                    float o[12];
+#pragma unroll
+                    for (int n = 0; n < 12; n += 4) {
+                        float acc[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
+#pragma unroll
+                        for (int k = 0; k < 12; ++k) {
+                            const float4 wv = *reinterpret_cast<const float4*>(wl + k * N + n);
+                            acc[0] = fmaf(xr[k], wv.x, acc[0]);
+                            acc[1] = fmaf(xr[k], wv.y, acc[1]);
+                            acc[2] = fmaf(xr[k], wv.z, acc[2]);
+                            acc[3] = fmaf(xr[k], wv.w, acc[3]);
+                        }
+                        o[n] = acc[0]; o[n + 1] = acc[1]; o[n + 2] = acc[2]; o[n + 3] = acc[3];
+                    }
+#pragma unroll
+                    for (int n = 0; n < 12; n += 4)
+                        t4[threadIdx.x * 3 + n / 4] = make_float4(o[n], o[n + 1], o[n + 2], o[n + 3]);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int e = k * 256 + threadIdx.x;
+                    if (e < nv) {
+                        float4 v = t4[e];
+                        if (r4 != nullptr) {
+                            const float4 rv = r4[r0 * 3 + e];
+                            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+                        }
+                        y4[r0 * 3 + e] = v;
+                    }
+                }
+            }
+            return;
+        }
+    }
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.rows; r += (int64_t)gridDim.x * blockDim.x) {
         // keep the LDS weight reads inside the loop: hoisted, K*N weights would not fit in VGPRs
         asm volatile("" ::: "memory");

@@ -619,6 +619,7 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (R * KS);
+    if (qpl == 2 && !bwd && WPB > MMNI_PK2_FWD_WPB) WPB = MMNI_PK2_FWD_WPB;
     if (WPB < 1) WPB = 1;
     const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;

@@ -100,6 +100,9 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
 #endif
+#ifndef MMNI_PK2_FWD_WPB
+#define MMNI_PK2_FWD_WPB 2    // windows per block of the two-query forward: two blocks share a CU
+#endif
 #ifndef MMNI_PK2_PAIRK
 #define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
 #endif
