@@ -602,7 +602,7 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
     const size_t T = (size_t)WPB * NPAD;
     if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
     if (packed)
-        return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * ((NH + 3) & ~3) * 4 +
+        return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * (NH == 2 ? 2 : (NH + 3) & ~3) * 4 +
                (size_t)Tsz * (NH + kDtabPad) * (kDtab32 ? 4 : 8) +
                (size_t)NH * 4;
     const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
@@ -645,14 +645,16 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
 }
 
 static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
-                    int& qpl) {
+                    int& qpl, int* hsplit = nullptr) {
     const int C = d->C;
     packed = false;
     qpl = 1;
-    int mf = 0, mb = 0, qf = 1, qb = 1;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb)) {
+    if (hsplit) *hsplit = 1;
+    int mf = 0, mb = 0, qf = 1, qb = 1, hb = 1;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb, hb)) {
         maxt = bwd ? mb : mf;
         qpl = bwd ? qb : qf;
+        if (hsplit && bwd) *hsplit = hb;
         packed = true;
         return 0;
     }
@@ -736,6 +738,7 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
     a.vmax = packed ? vmax : nullptr;   // the packed kernels fold max|v| into their K/V staging
+    a.hsplit = 1;
     rc = ensure_lds_attr(kf, cfg.lds);
     if (rc) return rc;
     void* args[] = {&a};
@@ -775,12 +778,26 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    int qpl = 1;
-    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl);
+    int qpl = 1, hs = 1;
+    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl, &hs);
     if (rc) return rc;
+    MMNI_ARG_CHECK(hs == 1 || (d->heads % hs == 0 && (d->heads / hs) % 2 == 0), "wattn_bwd: head groups");
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg, qpl);
+    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, true, packed, cfg, qpl);
     if (rc) return rc;
+    a.hsplit = hs;
+    if (hs > 1) {
+        // one block per (window, head group): the resident grid, a multiple of the group count
+        int64_t items = (int64_t)cfg.ngroups * hs;
+        int64_t grid = (int64_t)cfg.grid * hs;
+        const int64_t cap = (int64_t)kNumCU * (int)((160 * 1024) / cfg.lds < 2048 / cfg.threads
+                                                        ? (160 * 1024) / cfg.lds : 2048 / cfg.threads);
+        if (grid > cap) grid = cap;
+        if (grid > items) grid = items;
+        grid -= grid % hs;
+        MMNI_ARG_CHECK(grid >= hs, "wattn_bwd: empty head-group grid");
+        cfg.grid = (int)grid;
+    }
     MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");
     MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / 2) * cfg.KS, "wattn_bwd: two-row kernel launch shape");
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;

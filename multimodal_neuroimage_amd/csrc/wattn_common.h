@@ -74,6 +74,7 @@ struct WAArgs {
     unsigned int* maxbits;          // workspace tail: max|dout|, max|v| bits (fixed-point scale)
     int fix_shift;                  // bits the block-local fixed-point scale is lowered by (32-bit LDS sums)
     unsigned int* vmax;             // forward (packed kernels): running max|v| (float bits), or null
+    int hsplit;                     // two-row backward: head groups per window (blocks split the heads)
 };
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
@@ -103,6 +104,9 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK2_FWD_WPB
 #define MMNI_PK2_FWD_WPB 2    // windows per block of the two-query forward: two blocks share a CU
 #endif
+#ifndef MMNI_BWD_HSPLIT
+#define MMNI_BWD_HSPLIT 3     // two-row backward: blocks per window, one per head pair (1: all heads)
+#endif
 #ifndef MMNI_PK2_PAIRK
 #define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
 #endif
@@ -118,8 +122,9 @@ constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local tabl
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
+// hs_b: head groups of the backward kernel (> 1: each block takes C / hs_b channels of a window).
 int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
-                     int& qpl_b);
+                     int& qpl_b, int& hs_b);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the

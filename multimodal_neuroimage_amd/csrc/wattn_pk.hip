@@ -490,6 +490,7 @@ __device__ __forceinline__ void lds_row(f2 (&d)[C / 2], const float* s) {
 // position of float h of table row `row` (NHP floats per row, float4 chunks optionally swizzled)
 template <int NHP>
 __device__ __forceinline__ int tab_pos(int row, int h) {
+    if constexpr (NHP == 2) return row * 2 + h;   // two-head rows: one 8-B read, no swizzle
     constexpr int NCH = NHP / 4;   // float4 chunks per row; the swizzle needs a power of two
     const int c = h >> 2;
     const int cs = (kTabSwz && (NCH & (NCH - 1)) == 0) ? (c ^ ((row >> 3) & (NCH - 1))) : c;
@@ -499,6 +500,10 @@ __device__ __forceinline__ int tab_pos(int row, int h) {
 // table row (NHP floats, NHP % 4 == 0) -> NP float2
 template <int NP, int NHP>
 __device__ __forceinline__ void lds_tab(f2 (&d)[NP], const float* tab, int row) {
+    if constexpr (NHP == 2) {
+        d[0] = *reinterpret_cast<const f2*>(tab + row * 2);
+        return;
+    }
     float t[NHP];
 #pragma unroll
     for (int i = 0; i < NHP; i += 4) {
@@ -849,9 +854,9 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
 // LDS holds the bias table and its 64-bit gradient), 7 waves with up to 256 VGPRs each.
 // Kind 0 (scaled dot + table bias) only; WPB = 1.
 template <int C, int MAXT>
-__global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
+__global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAArgs a) {
     constexpr int HD = 2, NH = C / HD, NP = NH / 2;
-    constexpr int NHP = (NH + 3) & ~3;
+    constexpr int NHP = NH == 2 ? 2 : (NH + 3) & ~3;
     constexpr int DS = NH + kDtabPad;
     using dt_t = std::conditional_t<kDtab32, unsigned int, unsigned long long>;
     static_assert(NH % 2 == 0, "head pairs");
@@ -864,6 +869,11 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
     float* tab_s = reinterpret_cast<float*>(meta_s + NPAD);
     dt_t* dtab_s = reinterpret_cast<dt_t*>(tab_s + (size_t)g.Tsz * NHP);
 
+    // head groups (a.hsplit > 1): block b serves heads [h0, h0 + NH) of the NHT = NH * hsplit
+    // heads, for windows b / hsplit, b / hsplit + gridDim / hsplit, ...  Rows, lse and the table
+    // are addressed with the full head count; coff offsets the channel columns.
+    const int NHG = a.hsplit, hg = blockIdx.x % NHG, h0 = hg * NH, NHT = NH * NHG;
+    const int coff = h0 * HD;
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
     const bool lane_ok = r < NHALF;
@@ -871,7 +881,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
 
     for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
         const int row = e / NHP, h = e - row * NHP;
-        tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
+        tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NHT + h0 + h] * kLog2e : 0.f;
     }
     for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0;
     const int fexp = fix_exponent(a.maxbits, HD) - a.fix_shift;
@@ -880,7 +890,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
     const int nk = NPAD / KS;
     const f2 qscale = splat(a.scale * kLog2e);
 
-    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+    for (int grp = blockIdx.x / NHG; grp < a.ngroups; grp += gridDim.x / NHG) {
         const int w = grp;
         const bool active = lane_ok && (w < g.nwin);
         const bool masked = group_masked(g, grp, 1, NPAD);
@@ -908,7 +918,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
             for (int m = 0; m < KVPL; ++m) {
                 const int c = p + 4 * m, u = c / (2 * (C / 4)), cc = c - u * 2 * (C / 4);
                 const bool isv = cc >= C / 4;
-                const float* src = isv ? a.v + row[u] * a.vs : a.k + row[u] * a.ks;
+                const float* src = (isv ? a.v + row[u] * a.vs : a.k + row[u] * a.ks) + coff;
                 kvc[m] = c < KVCH ? *reinterpret_cast<const float4*>(src + 4 * (cc - (isv ? C / 4 : 0)))
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
             }
@@ -917,10 +927,10 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
         for (int u = 0; u < 2; ++u) {
             if (active) {
                 const int64_t rw = row[u];
-                load_pk<C>(aq[u], a.q + rw * a.qs);
+                load_pk<C>(aq[u], a.q + rw * a.qs + coff);
                 f2 orow[C / 2];
-                load_pk<C>(dO[u], a.dout + rw * a.os);
-                load_pk<C>(orow, a.o + rw * a.os);
+                load_pk<C>(dO[u], a.dout + rw * a.os + coff);
+                load_pk<C>(orow, a.o + rw * a.os + coff);
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
                     aq[u][2 * P] *= qscale;
@@ -929,7 +939,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
                     ndl[u][P] = dd * splat(-fs);
                     dO[u][2 * P] *= splat(fs);
                     dO[u][2 * P + 1] *= splat(fs);
-                    lse2[u][P] = (f2){a.lse[rw * NH + 2 * P], a.lse[rw * NH + 2 * P + 1]} * kLog2e;
+                    lse2[u][P] = (f2){a.lse[rw * NHT + h0 + 2 * P], a.lse[rw * NHT + h0 + 2 * P + 1]} * kLog2e;
                 }
             } else {
 #pragma unroll
@@ -1067,7 +1077,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
             }
             if (active && p == 0) {
 #pragma unroll
-                for (int u = 0; u < 2; ++u) store_nat<C>(a.dq + row[u] * a.qs, dqa[u], a.scale * ifs);
+                for (int u = 0; u < 2; ++u) store_nat<C>(a.dq + row[u] * a.qs + coff, dqa[u], a.scale * ifs);
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -1075,8 +1085,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
                     lds_row<C>(kr[u], rowb + (size_t)(rr + u * NHALF) * 2 * C);
                     lds_row<C>(vr[u], rowb + (size_t)(rr + u * NHALF) * 2 * C + C);
                 } else if (active) {
-                    load_pk<C>(kr[u], a.k + row[u] * a.ks);
-                    load_pk<C>(vr[u], a.v + row[u] * a.vs);
+                    load_pk<C>(kr[u], a.k + row[u] * a.ks + coff);
+                    load_pk<C>(vr[u], a.v + row[u] * a.vs + coff);
                 } else {
 #pragma unroll
                     for (int i = 0; i < C / 2; ++i) { kr[u][i] = splat(0.f); vr[u][i] = splat(0.f); }
@@ -1177,8 +1187,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
             if (active && p == 0) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
-                    store_nat<C>(a.dv + row[u] * a.vs, dva[u], ifs);
-                    store_nat<C>(a.dk + row[u] * a.ks, dka[u], kLn2 * ifs);
+                    store_nat<C>(a.dv + row[u] * a.vs + coff, dva[u], ifs);
+                    store_nat<C>(a.dk + row[u] * a.ks + coff, dka[u], kLn2 * ifs);
                 }
             }
         }
@@ -1187,7 +1197,9 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk2_kernel(WAArgs a) {
     __syncthreads();
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
         const dt_t v = dtab_s[(e / NH) * DS + e % NH];
-        if (v != 0) atomicAdd(&a.dtab_fix[e], kDtab32 ? (unsigned long long)(long long)(int)v : (unsigned long long)v);
+        if (v != 0)
+            atomicAdd(&a.dtab_fix[(e / NH) * NHT + h0 + e % NH],
+                      kDtab32 ? (unsigned long long)(long long)(int)v : (unsigned long long)v);
     }
 }
 
@@ -1214,16 +1226,20 @@ static void* pk2_fwd(int kind) {
 // qpl_f / qpl_b: rows per lane of the forward / backward (2: the pk2 kernels, windows of even N;
 // the two-row backward needs one window per block, N > 128).
 int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
-                     int& qpl_b) {
+                     int& qpl_b, int& hs_b) {
     const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
     const bool two_b = MMNI_BWD_QPL == 2 && kind == 0 && N % 2 == 0 && N > 128;
     qpl_f = two ? 2 : 1;
     qpl_b = 1;
+    hs_b = 1;
     if (C == 12) {
         kf = two ? pk2_fwd<12, 512>(kind) : pk_fwd<12, 512>(kind);
         maxt_f = 512;
         if (two_b) {
-            kb = reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<12, 512>);
+            // MMNI_BWD_HSPLIT 3: one block per (window, head pair), 4 channels each
+            kb = MMNI_BWD_HSPLIT == 3 ? reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<4, 512>)
+                                      : reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<12, 512>);
+            hs_b = MMNI_BWD_HSPLIT == 3 ? 3 : 1;
             maxt_b = 512;
             qpl_b = 2;
         } else {

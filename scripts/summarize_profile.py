@@ -27,8 +27,8 @@ def bench_key(name):
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
     m = re.search(r"mmni::wattn_bwd_pk2_kernel<(\d+), \d+>", name)   # kind 0 only
-    if m:
-        return f"wattn_bwd_k0_C{m.group(1)}"
+    if m:   # <4, .>: the head-pair split of the C = 12 layer (three blocks per window)
+        return f"wattn_bwd_k0_C{12 if m.group(1) == '4' else m.group(1)}"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
     if m:
         return f"{m.group(1)}_hd{m.group(2)}"
