@@ -794,8 +794,8 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                                                         ? (160 * 1024) / cfg.lds : 2048 / cfg.threads);
         if (grid > cap) grid = cap;
         if (grid > items) grid = items;
-        grid -= grid % hs;
-        MMNI_ARG_CHECK(grid >= hs, "wattn_bwd: empty head-group grid");
+        grid -= grid % (8 * hs);   // XCD-aligned head groups (see wattn_bwd_pk2_kernel)
+        if (grid < 8 * hs) grid = 8 * hs;   // tiny inputs: surplus blocks find no window
         cfg.grid = (int)grid;
     }
     MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");

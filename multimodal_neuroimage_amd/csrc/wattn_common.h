@@ -107,6 +107,9 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_BWD_HSPLIT
 #define MMNI_BWD_HSPLIT 3     // two-row backward: blocks per window, one per head pair (1: all heads)
 #endif
+#ifndef MMNI_HS_XCD
+#define MMNI_HS_XCD 1         // head-group blocks of a window on one XCD
+#endif
 #ifndef MMNI_PK2_PAIRK
 #define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
 #endif

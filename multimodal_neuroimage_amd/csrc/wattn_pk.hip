@@ -872,7 +872,14 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
     // head groups (a.hsplit > 1): block b serves heads [h0, h0 + NH) of the NHT = NH * hsplit
     // heads, for windows b / hsplit, b / hsplit + gridDim / hsplit, ...  Rows, lse and the table
     // are addressed with the full head count; coff offsets the channel columns.
-    const int NHG = a.hsplit, hg = blockIdx.x % NHG, h0 = hg * NH, NHT = NH * NHG;
+    // The NHG blocks of a window sit 8 block indices apart: blocks are dealt round-robin over the
+    // 8 XCDs, so they share one XCD's L2 (one HBM fetch of the window's rows, and their 16-B
+    // column pieces of dq / dk / dv merge there).  The host makes the grid a multiple of 8 NHG.
+    const int NHG = a.hsplit;
+    const int xslot = blockIdx.x >> 3;
+    const int hg = NHG > 1 ? (MMNI_HS_XCD ? xslot % NHG : blockIdx.x % NHG) : 0;
+    const int wfirst = NHG > 1 ? (MMNI_HS_XCD ? (xslot / NHG) * 8 + (blockIdx.x & 7) : blockIdx.x / NHG) : blockIdx.x;
+    const int h0 = hg * NH, NHT = NH * NHG;
     const int coff = h0 * HD;
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -890,7 +897,7 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
     const int nk = NPAD / KS;
     const f2 qscale = splat(a.scale * kLog2e);
 
-    for (int grp = blockIdx.x / NHG; grp < a.ngroups; grp += gridDim.x / NHG) {
+    for (int grp = wfirst; grp < a.ngroups; grp += gridDim.x / NHG) {
         const int w = grp;
         const bool active = lane_ok && (w < g.nwin);
         const bool masked = group_masked(g, grp, 1, NPAD);
