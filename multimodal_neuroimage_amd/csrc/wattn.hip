@@ -592,6 +592,7 @@ struct WAKernels {
 
 struct WAConfig {
     int KS, WPB, NPAD, threads, ngroups, grid;
+    int cap;   // block cap of the launch (resident blocks; x4 for the forward)
     size_t lds;
 };
 
@@ -639,9 +640,20 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     // forward: a few groups per block amortise the table staging; backward: one flush
     // of the table gradient per block, so stay at one resident wave of blocks.
     const int cap = bwd ? resident : resident * 4;
+    cfg.cap = cap;
     cfg.grid = cfg.ngroups < cap ? cfg.ngroups : cap;
     cfg.lds = lds;
     return 0;
+}
+
+// Grid of a head-split launch: (window group, head group) items up to the plan's block cap, a
+// multiple of 8 x groups (the kernels deal a group's blocks to one XCD).
+static int head_group_grid(const WAConfig& cfg, int hs) {
+    const int64_t items = (int64_t)cfg.ngroups * hs;
+    int64_t grid = items < cfg.cap ? items : cfg.cap;
+    grid -= grid % (8 * hs);
+    if (grid < 8 * hs) grid = 8 * hs;   // tiny inputs: surplus blocks find no window
+    return (int)grid;
 }
 
 static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
@@ -650,11 +662,11 @@ static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*
     packed = false;
     qpl = 1;
     if (hsplit) *hsplit = 1;
-    int mf = 0, mb = 0, qf = 1, qb = 1, hb = 1;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb, hb)) {
+    int mf = 0, mb = 0, qf = 1, qb = 1, hb = 1, hf = 1;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb, hb, hf)) {
         maxt = bwd ? mb : mf;
         qpl = bwd ? qb : qf;
-        if (hsplit && bwd) *hsplit = hb;
+        if (hsplit) *hsplit = bwd ? hb : hf;
         packed = true;
         return 0;
     }
@@ -729,16 +741,18 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    int qpl = 1;
-    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl);
+    int qpl = 1, hs = 1;
+    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl, &hs);
     if (rc) return rc;
+    MMNI_ARG_CHECK(hs == 1 || (d->heads % hs == 0 && (d->heads / hs) % 2 == 0), "wattn_fwd: head groups");
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg, qpl);
+    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, false, packed, cfg, qpl);
     if (rc) return rc;
+    if (hs > 1) cfg.grid = head_group_grid(cfg, hs);
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
     a.vmax = packed ? vmax : nullptr;   // the packed kernels fold max|v| into their K/V staging
-    a.hsplit = 1;
+    a.hsplit = hs;
     rc = ensure_lds_attr(kf, cfg.lds);
     if (rc) return rc;
     void* args[] = {&a};
@@ -786,18 +800,7 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     rc = plan(a.g, d->C / hs, d->heads / hs, maxt, true, packed, cfg, qpl);
     if (rc) return rc;
     a.hsplit = hs;
-    if (hs > 1) {
-        // one block per (window, head group): the resident grid, a multiple of the group count
-        int64_t items = (int64_t)cfg.ngroups * hs;
-        int64_t grid = (int64_t)cfg.grid * hs;
-        const int64_t cap = (int64_t)kNumCU * (int)((160 * 1024) / cfg.lds < 2048 / cfg.threads
-                                                        ? (160 * 1024) / cfg.lds : 2048 / cfg.threads);
-        if (grid > cap) grid = cap;
-        if (grid > items) grid = items;
-        grid -= grid % (8 * hs);   // XCD-aligned head groups (see wattn_bwd_pk2_kernel)
-        if (grid < 8 * hs) grid = 8 * hs;   // tiny inputs: surplus blocks find no window
-        cfg.grid = (int)grid;
-    }
+    if (hs > 1) cfg.grid = head_group_grid(cfg, hs);
     MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");
     MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / 2) * cfg.KS, "wattn_bwd: two-row kernel launch shape");
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;

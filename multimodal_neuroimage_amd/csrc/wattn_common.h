@@ -110,6 +110,9 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_HS_XCD
 #define MMNI_HS_XCD 1         // head-group blocks of a window on one XCD
 #endif
+#ifndef MMNI_FWD_HSPLIT
+#define MMNI_FWD_HSPLIT 1     // two-query forward head groups (3 measured 1.86 vs 1.66 ms: kept at 1)
+#endif
 #ifndef MMNI_PK2_PAIRK
 #define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
 #endif
@@ -125,9 +128,9 @@ constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local tabl
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
-// hs_b: head groups of the backward kernel (> 1: each block takes C / hs_b channels of a window).
+// hs_b / hs_f: head groups of the backward / forward kernel (> 1: each block takes C / hs channels).
 int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
-                     int& qpl_b, int& hs_b);
+                     int& qpl_b, int& hs_b, int& hs_f);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the

@@ -267,20 +267,27 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
     int2* meta_s = reinterpret_cast<int2*>(kv_s + (size_t)WPB * NPAD * 2 * C);  // [WPB*NPAD]
     float* tab_s = reinterpret_cast<float*>(meta_s + WPB * NPAD);     // [Tsz][NH]
 
+    // head groups (a.hsplit > 1): as in wattn_bwd_pk2_kernel, the NHG blocks of a window group
+    // sit 8 block indices apart (one XCD) and take heads [h0, h0 + NH) of NHT
+    const int NHG = a.hsplit;
+    const int xslot = blockIdx.x >> 3;
+    const int hg = NHG > 1 ? xslot % NHG : 0;
+    const int gfirst = NHG > 1 ? (xslot / NHG) * 8 + (blockIdx.x & 7) : blockIdx.x;
+    const int h0 = hg * NH, NHT = NH * NHG, coff = h0 * HD;
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
     const int wl = r / NHALF, t = r - wl * NHALF;
     const int wl_c = wl < WPB ? wl : WPB - 1;
 
-    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[(e / NH) * NHT + h0 + e % NH] * kLog2e;
 
     f2 tau2[NP];
 #pragma unroll
     for (int P = 0; P < NP; ++P)
-        tau2[P] = (KIND == 1) ? (f2){a.tau[2 * P], a.tau[2 * P + 1]} * kLog2e : splat(a.scale * kLog2e);
+        tau2[P] = (KIND == 1) ? (f2){a.tau[h0 + 2 * P], a.tau[h0 + 2 * P + 1]} * kLog2e : splat(a.scale * kLog2e);
 
     float vabs = 0.f;
-    for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+    for (int grp = gfirst; grp < a.ngroups; grp += gridDim.x / NHG) {
         for (int e = tid; e < WPB * NPAD; e += blockDim.x) {
             const int w2 = e / NPAD, t2 = e - w2 * NPAD;
             const int w = grp * WPB + w2;
@@ -288,8 +295,8 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
             int2 mt;
             if (t2 < N && w < g.nwin) {
                 const TokenInfo ti = token_info(g, w, t2);
-                load_row<C>(kr, a.k + ti.row * a.ks);
-                load_row<C>(vr, a.v + ti.row * a.vs);
+                load_row<C>(kr, a.k + ti.row * a.ks + coff);
+                load_row<C>(vr, a.v + ti.row * a.vs + coff);
 #pragma unroll
                 for (int c = 0; c < C; ++c) vabs = fmaxf(vabs, fabsf(vr[c]));
                 if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(kr, nrm); }
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
                 row[u] = ti.row;
                 cq[u] = ti.code + g.off;
                 rq[u] = ti.rc;
-                load_row<C>(qr, a.q + ti.row * a.qs);
+                load_row<C>(qr, a.q + ti.row * a.qs + coff);
                 if (KIND == 1) { float nrm[NH]; normalize_heads<C, HD>(qr, nrm); }
             } else {
 #pragma unroll
@@ -426,12 +433,12 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
                     const f2 inv = (f2){1.0f / l[u][P].x, 1.0f / l[u][P].y};
                     op[2 * P] = acc[u][2 * P] * inv;
                     op[2 * P + 1] = acc[u][2 * P + 1] * inv;
-                    a.lse[row[u] * NH + 2 * P] = (m[u][P].x + fast_log2(l[u][P].x)) * kLn2;
-                    a.lse[row[u] * NH + 2 * P + 1] = (m[u][P].y + fast_log2(l[u][P].y)) * kLn2;
+                    a.lse[row[u] * NHT + h0 + 2 * P] = (m[u][P].x + fast_log2(l[u][P].x)) * kLn2;
+                    a.lse[row[u] * NHT + h0 + 2 * P + 1] = (m[u][P].y + fast_log2(l[u][P].y)) * kLn2;
                 }
                 float o[C];
                 unpack_row<C>(o, op);
-                store_row<C>(a.out + row[u] * a.os, o);
+                store_row<C>(a.out + row[u] * a.os + coff, o);
             }
         }
         __syncthreads();
@@ -1233,14 +1240,17 @@ static void* pk2_fwd(int kind) {
 // qpl_f / qpl_b: rows per lane of the forward / backward (2: the pk2 kernels, windows of even N;
 // the two-row backward needs one window per block, N > 128).
 int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
-                     int& qpl_b, int& hs_b) {
+                     int& qpl_b, int& hs_b, int& hs_f) {
     const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
     const bool two_b = MMNI_BWD_QPL == 2 && kind == 0 && N % 2 == 0 && N > 128;
     qpl_f = two ? 2 : 1;
     qpl_b = 1;
     hs_b = 1;
+    hs_f = 1;
     if (C == 12) {
-        kf = two ? pk2_fwd<12, 512>(kind) : pk_fwd<12, 512>(kind);
+        // MMNI_FWD_HSPLIT 3: the two-query forward per (window group, head pair)
+        kf = two ? (MMNI_FWD_HSPLIT == 3 ? pk2_fwd<4, 512>(kind) : pk2_fwd<12, 512>(kind)) : pk_fwd<12, 512>(kind);
+        if (two) hs_f = MMNI_FWD_HSPLIT == 3 ? 3 : 1;
         maxt_f = 512;
         if (two_b) {
             // MMNI_BWD_HSPLIT 3: one block per (window, head pair), 4 channels each
