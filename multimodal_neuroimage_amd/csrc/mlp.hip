@@ -212,12 +212,19 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
 // ------------------------------------------------------------------------------------
 constexpr int kBwdWaves = 4;   // waves per block (LDS transpose slab per wave)
 
+#ifndef MMNI_MLP_BWD_WLDS
+#define MMNI_MLP_BWD_WLDS 1
+#endif
+constexpr bool kWLds = MMNI_MLP_BWD_WLDS;
+#ifndef MMNI_LN_MLP_BWD_OCC
+#define MMNI_LN_MLP_BWD_OCC 3
+#endif
 #ifndef MMNI_MLP_BWD_OCC
 #define MMNI_MLP_BWD_OCC 3   // min waves per SIMD (caps VGPRs at 168)
 #endif
 // (the LN variant carries ~20 more live values: 2 waves per SIMD, no spills)
 template <bool LN>
-__global__ __launch_bounds__(256, LN ? 2 : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs a) {
+__global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs a) {
     __shared__ float tr[kBwdWaves][2][16][H + 4];   // per wave: g and dpre as [token][hidden]
     const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
     const int wib = threadIdx.x >> 6;
@@ -226,18 +233,40 @@ __global__ __launch_bounds__(256, LN ? 2 : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel
     const TileIO io{a.rows, li, lg};
     float w1a[HT][CS], w2ta[HT][CS], w1ta[HT][4];
     f4 b1c[HT];
+    // MMNI_MLP_BWD_WLDS: the 42 per-lane weight values live in LDS ([value][lane]: conflict-free)
+    // and are re-read per tile, which frees their VGPRs for a third wave per SIMD
+    constexpr int NWV = HT * (2 * CS + 8);
+    __shared__ float wv_s[kWLds ? NWV * 64 : 1];
+    auto wload = [&]() {
 #pragma unroll
-    for (int ht = 0; ht < HT; ++ht) {
+        for (int ht = 0; ht < HT; ++ht) {
 #pragma unroll
-        for (int s = 0; s < CS; ++s) {
-            w1a[ht][s] = a.w1[(ht * 16 + li) * C + 4 * s + lg];      // W1[hid][c]
-            w2ta[ht][s] = a.w2[(4 * s + lg) * H + ht * 16 + li];     // W2^T[hid][o] = W2[o][hid]
+            for (int s = 0; s < CS; ++s) {
+                w1a[ht][s] = a.w1[(ht * 16 + li) * C + 4 * s + lg];      // W1[hid][c]
+                w2ta[ht][s] = a.w2[(4 * s + lg) * H + ht * 16 + li];     // W2^T[hid][o] = W2[o][hid]
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w1ta[ht][i] = li < C ? a.w1[(ht * 16 + 4 * lg + i) * C + li] : 0.f;   // W1^T[c][hid]
+                b1c[ht][i] = a.b1 ? a.b1[ht * 16 + 4 * lg + i] : 0.f;
+            }
         }
+    };
+    auto wslot = [&](int ht, int k) -> float& { return wv_s[(ht * (2 * CS + 8) + k) * 64 + lane]; };
+    if constexpr (kWLds) {
+        if (wib == 0) {
+            wload();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            w1ta[ht][i] = li < C ? a.w1[(ht * 16 + 4 * lg + i) * C + li] : 0.f;   // W1^T[c][hid]
-            b1c[ht][i] = a.b1 ? a.b1[ht * 16 + 4 * lg + i] : 0.f;
+            for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+                for (int s = 0; s < CS; ++s) { wslot(ht, s) = w1a[ht][s]; wslot(ht, CS + s) = w2ta[ht][s]; }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { wslot(ht, 2 * CS + i) = w1ta[ht][i]; wslot(ht, 2 * CS + 4 + i) = b1c[ht][i]; }
+            }
         }
+        __syncthreads();
+    } else {
+        wload();
     }
     f4 dw1[HT], dw2[HT];   // dW1 tile ht: rows hid, cols c;  dW2 tile ht: rows o, cols hid
     f4 db1[HT];            // per-lane partial column sums of dpre (rows hid, this lane's tokens)
@@ -266,6 +295,16 @@ __global__ __launch_bounds__(256, LN ? 2 : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel
     const int64_t tiles = (a.rows + 15) / 16;
     for (int64_t tile = wave; tile < tiles; tile += nwaves) {
         const int64_t t0 = tile * 16;
+        if constexpr (kWLds) {
+            asm volatile("" ::: "memory");   // keep the weight reads in the loop (not hoisted)
+#pragma unroll
+            for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+                for (int s = 0; s < CS; ++s) { w1a[ht][s] = wslot(ht, s); w2ta[ht][s] = wslot(ht, CS + s); }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { w1ta[ht][i] = wslot(ht, 2 * CS + i); b1c[ht][i] = wslot(ht, 2 * CS + 4 + i); }
+            }
+        }
         float xb[CS], dyb[CS], xa[4], dya[4];
         io.load_fm(a.x, t0, xb);
         io.load_fm(a.dy, t0, dyb);
