@@ -614,7 +614,7 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
     const int chunk = packed ? (qpl == 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl == 2 ? (bwd ? 4 : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    int KS = qpl == 4 ? 8 : qpl == 2 ? (bwd ? 4 : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
@@ -622,9 +622,11 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     int WPB = target / (R * KS);
     if (qpl == 2 && !bwd && WPB > MMNI_PK2_FWD_WPB) WPB = MMNI_PK2_FWD_WPB;
     if (WPB < 1) WPB = 1;
-    const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
+    // the quad backward walks N / 4 bases per slice and stages exactly the window's rows
+    const int NPAD = qpl == 4 ? N : (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
-    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz);
+    // the quad backward stages the scaled q / dO rows beside K / V (no restage between its passes)
+    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) + (qpl == 4 ? (size_t)NPAD * 2 * C * 4 : 0);
     MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
     cfg.KS = KS;
     cfg.WPB = WPB;
@@ -663,7 +665,7 @@ static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*
     qpl = 1;
     if (hsplit) *hsplit = 1;
     int mf = 0, mb = 0, qf = 1, qb = 1, hb = 1, hf = 1;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf, qb, hb, hf)) {
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, d->wd % 2 == 0 && d->wh % 2 == 0, kf, kb, mf, mb, qf, qb, hb, hf)) {
         maxt = bwd ? mb : mf;
         qpl = bwd ? qb : qf;
         if (hsplit) *hsplit = bwd ? hb : hf;
@@ -801,8 +803,10 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     if (rc) return rc;
     a.hsplit = hs;
     if (hs > 1) cfg.grid = head_group_grid(cfg, hs);
-    MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: two-row kernel needs one window per block");
-    MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / 2) * cfg.KS, "wattn_bwd: two-row kernel launch shape");
+    MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: multi-row kernels need one window per block");
+    MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / qpl) * cfg.KS, "wattn_bwd: multi-row kernel launch shape");
+    MMNI_ARG_CHECK(qpl != 4 || (a.g.N % 4 == 0 && a.g.wd % 2 == 0 && a.g.wh % 2 == 0 && cfg.KS == 8 && hs == 3),
+                   "wattn_bwd: quad kernel geometry");
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;

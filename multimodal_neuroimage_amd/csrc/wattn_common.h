@@ -96,7 +96,7 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
 #endif
 #ifndef MMNI_BWD_QPL
-#define MMNI_BWD_QPL 2        // rows per lane of the packed C = 12 backward (kind 0)
+#define MMNI_BWD_QPL 2        // rows per lane of the packed C = 12 backward (kind 0): 2, or 4 (quads; wd, wh even)
 #endif
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
@@ -129,7 +129,7 @@ constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (pa
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
 // hs_b / hs_f: head groups of the backward / forward kernel (> 1: each block takes C / hs channels).
-int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
+int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
                      int& qpl_b, int& hs_b, int& hs_f);
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a

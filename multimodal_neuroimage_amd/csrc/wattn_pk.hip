@@ -1217,6 +1217,301 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
     }
 }
 
+// ------------------------------------------------------------------------------------
+// backward, four rows per lane
+// ------------------------------------------------------------------------------------
+// wattn_bwd_pk2_kernel with each lane carrying a quad of its window: tokens t, t + D1, t + D2 and
+// t + D1 + D2, where D1 moves by half the window's planes and D2 by half its rows (wd, wh even).
+// The relative code is linear in (i, j, k), so member m = a + 2c of a query quad and member
+// n = a' + 2c' of a key quad read table row  base + (a - a') d1 + (c - c') d2 :  16 pairs touch
+// 9 rows.  Pass A (lane = query quad) reads one key quad (4 K/V rows) and 9 table rows per 16
+// pairs and issues 9 table-gradient atomics per head (two-row kernel: 8 K/V rows, 12 table rows,
+// 12 atomics); pass B (lane = key quad) reads 4 query rows and 9 table rows per 16 pairs (8 and
+// 16).  N/4 quads x KS = 8 key slices: 432 threads at 6^3.  Kind 0, C = 4 (one head pair per
+// block, head groups as in wattn_bwd_pk2_kernel), one window per block.
+#ifndef MMNI_PK4_WAVES
+#define MMNI_PK4_WAVES 4
+#endif
+#ifndef MMNI_PK4_TB9
+#define MMNI_PK4_TB9 1   // pass B holds the 9 table rows of a quad pair (0: 4 reads per query row)
+#endif
+#ifndef MMNI_PK4_OPAQUE
+#define MMNI_PK4_OPAQUE 1
+#endif
+#ifndef MMNI_PK4_SCHED
+#define MMNI_PK4_SCHED 1
+#endif
+template <int C, int MAXT>
+__global__ __launch_bounds__(MAXT, MMNI_PK4_WAVES) void wattn_bwd_pk4_kernel(WAArgs a) {
+    constexpr int HD = 2, NH = C / HD, NP = NH / 2;
+    constexpr int NHP = NH == 2 ? 2 : (NH + 3) & ~3;
+    constexpr int DS = NH + kDtabPad;
+    using dt_t = unsigned long long;
+    static_assert(C == 4 && NP == 1, "one head pair per block: a K, V, Q or dO row is one float4");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int N = g.N, KS = a.KS, NQ = N / 4;
+    float* kv_s = smem;                                   // [N][2C]: pk k | pk v
+    float* qg_s = smem + (size_t)N * 2 * C;               // [N][2C]: pk q*scale | pk dO*2^S
+    float* rs_s = smem + (size_t)N * 4 * C;               // [N][2NH]: lse2 | -delta*2^S
+    int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)N * 2 * NH);
+    float* tab_s = reinterpret_cast<float*>(meta_s + N);
+    dt_t* dtab_s = reinterpret_cast<dt_t*>(tab_s + (size_t)g.Tsz * NHP);
+
+    const int NHG = a.hsplit;
+    const int xslot = blockIdx.x >> 3;
+    const int hg = NHG > 1 ? xslot % NHG : 0;
+    const int wfirst = NHG > 1 ? (xslot / NHG) * 8 + (blockIdx.x & 7) : blockIdx.x;
+    const int h0 = hg * NH, NHT = NH * NHG;
+    const int coff = h0 * HD;
+    const int tid = threadIdx.x;
+    const int r = tid / KS, p = tid - r * KS;
+    const bool lane_ok = r < NQ;
+    const int rr = lane_ok ? r : 0;
+    // quad geometry (window-independent): base b -> token, member shifts in tokens and in codes
+    const int hw2 = (g.wh >> 1) * g.ww, pl = g.wh * g.ww;
+    const int D1 = (g.wd >> 1) * pl, D2 = hw2;
+    const int d1 = (g.wd >> 1) * g.tw, d2 = (g.wh >> 1) * g.th;
+    auto quad_tok = [&](int b) {
+        const int z = b / hw2;
+        return z * pl + (b - z * hw2);
+    };
+    auto member = [&](int t, int m) { return t + (m & 1) * D1 + (m >> 1) * D2; };
+    auto tab_row = [&](int t0, int ti) { return t0 + (ti / 3 - 1) * d1 + (ti % 3 - 1) * d2; };
+
+    for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
+        const int row = e / NHP, h = e - row * NHP;
+        tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NHT + h0 + h] * kLog2e : 0.f;
+    }
+    for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0;
+    const int fexp = fix_exponent(a.maxbits, HD) - a.fix_shift;
+    const float fs = exp2f((float)fexp);
+    const float ifs = exp2f((float)-fexp);
+    const float qsc = a.scale * kLog2e;
+    const int t0i = quad_tok(rr);
+    const int nb = (NQ - p + KS - 1) / KS;   // bases p, p + KS, ... < NQ of this lane's slice
+
+    for (int w = wfirst; w < a.ngroups; w += gridDim.x / NHG) {
+        // t0 is opaque per window: keeps the compiler from hoisting every LDS / row address
+        // derived from it out of the window loop (they would stay live across both passes)
+        int t0 = t0i;
+        if (MMNI_PK4_OPAQUE) asm volatile("" : "+v"(t0));
+        // the member this lane stages (p >> 1) and stores (p < 4: member p)
+        const int ts = member(t0, p >> 1), tw = member(t0, p & 3);
+        const bool masked = group_masked(g, w, 1, N);
+        int cq0, rcq[4];
+        {
+            const TokenInfo ti = token_info(g, w, t0);
+            cq0 = ti.code + g.off;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rcq[u] = masked ? token_info(g, w, member(t0, u)).rc : 0;
+        // ---- staging: lane p of a quad moves member p / 2's rows; even lanes K, V and Q,
+        //      odd lanes dO, O and lse (-> dO*2^S, -delta*2^S, lse2)
+        if (lane_ok) {
+            const TokenInfo ti = token_info(g, w, ts);
+            const int64_t rw = ti.row;
+            if ((p & 1) == 0) {
+                const float4 kk = *reinterpret_cast<const float4*>(a.k + rw * a.ks + coff);
+                const float4 vv = *reinterpret_cast<const float4*>(a.v + rw * a.vs + coff);
+                const float4 qq = *reinterpret_cast<const float4*>(a.q + rw * a.qs + coff);
+                *reinterpret_cast<float4*>(kv_s + (size_t)ts * 2 * C) = make_float4(kk.x, kk.z, kk.y, kk.w);
+                *reinterpret_cast<float4*>(kv_s + (size_t)ts * 2 * C + C) = make_float4(vv.x, vv.z, vv.y, vv.w);
+                *reinterpret_cast<float4*>(qg_s + (size_t)ts * 2 * C) =
+                    make_float4(qq.x * qsc, qq.z * qsc, qq.y * qsc, qq.w * qsc);
+                meta_s[ts] = make_int2(ti.code | (ti.rc << 16), 0);
+            } else {
+                const float4 gg = *reinterpret_cast<const float4*>(a.dout + rw * a.os + coff);
+                const float4 oo = *reinterpret_cast<const float4*>(a.o + rw * a.os + coff);
+                const float2 ls = *reinterpret_cast<const float2*>(a.lse + rw * NHT + h0);
+                *reinterpret_cast<float4*>(qg_s + (size_t)ts * 2 * C + C) =
+                    make_float4(gg.x * fs, gg.z * fs, gg.y * fs, gg.w * fs);
+                // natural row (h0 c0, h0 c1, h1 c0, h1 c1): delta per head
+                const float dl0 = fmaf(oo.x, gg.x, oo.y * gg.y), dl1 = fmaf(oo.z, gg.z, oo.w * gg.w);
+                *reinterpret_cast<float4*>(rs_s + (size_t)ts * 2 * NH) =
+                    make_float4(ls.x * kLog2e, ls.y * kLog2e, -dl0 * fs, -dl1 * fs);
+            }
+        }
+        __syncthreads();
+
+        // ================= pass A: query quad -> dq, dtable
+        {
+            f2 aq[4][C / 2], dO[4][C / 2], lse2[4], ndl[4], dqa[4][C / 2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = member(t0, u);
+                lds_row<C>(aq[u], qg_s + (size_t)t * 2 * C);
+                lds_row<C>(dO[u], qg_s + (size_t)t * 2 * C + C);
+                const float4 x = *reinterpret_cast<const float4*>(rs_s + (size_t)t * 2 * NH);
+                lse2[u] = (f2){x.x, x.y};
+                ndl[u] = (f2){x.z, x.w};
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) dqa[u][i] = splat(0.f);
+            }
+#pragma unroll 1
+            for (int n = 0; n < ((MMNI_ABL & 4) ? 0 : nb); ++n) {
+                const int k0 = quad_tok(p + KS * n);
+                int2 mk[4];
+                mk[0] = meta_s[k0];
+                if (masked) {
+#pragma unroll
+                    for (int m = 1; m < 4; ++m) mk[m] = meta_s[member(k0, m)];
+                } else {
+                    mk[1] = mk[2] = mk[3] = mk[0];
+                }
+                const int tix0 = cq0 - (mk[0].x & 0xffff);
+                f2 tb[9], acc[10];
+#pragma unroll
+                for (int ti = 0; ti < 9; ++ti) {
+                    lds_tab<1, NHP>(*reinterpret_cast<f2(*)[1]>(&tb[ti]), tab_s, tab_row(tix0, ti));
+                    acc[ti] = splat(0.f);
+                }
+                acc[9] = splat(0.f);
+#pragma unroll
+                for (int kn = 0; kn < 4; ++kn) {
+                    if (MMNI_PK4_SCHED) __builtin_amdgcn_sched_barrier(0);   // one key row in flight
+                    const int kt = member(k0, kn);
+                    f2 kj[C / 2], vj[C / 2];
+                    lds_row<C>(kj, kv_s + (size_t)kt * 2 * C);
+                    lds_row<C>(vj, kv_s + (size_t)kt * 2 * C + C);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const int ti = ((m & 1) - (kn & 1) + 1) * 3 + ((m >> 1) - (kn >> 1) + 1);
+                        const int ai = (ti == 4 && m >= 2) ? 9 : ti;
+                        f2 base = tb[ti] - lse2[m];
+                        if (masked) base += splat(((mk[kn].x >> 16) == rcq[m] ? 0.f : kMask2) + __int_as_float(mk[kn].y));
+                        f2 sc = pfma(aq[m][0], kj[0], base);
+                        sc = pfma(aq[m][1], kj[1], sc);
+                        const f2 pr = exp2_2(sc);
+                        f2 tt = pfma(dO[m][0], vj[0], ndl[m]);
+                        tt = pfma(dO[m][1], vj[1], tt);
+                        const f2 dsv = pr * tt;
+                        acc[ai] += dsv;
+                        dqa[m][0] = pfma(dsv, kj[0], dqa[m][0]);
+                        dqa[m][1] = pfma(dsv, kj[1], dqa[m][1]);
+                    }
+                }
+                // each accumulator holds at most two contributions (|sum| < 2^31 after scaling);
+                // the centre row's four are rounded as two sums and added in 64 bits
+                if (!(MMNI_ABL & 1) && lane_ok) {
+#pragma unroll
+                    for (int ti = 0; ti < 9; ++ti) {
+                        dt_t* dtp = dtab_s + tab_row(tix0, ti) * DS;
+                        long long vx = fix_round(acc[ti].x), vy = fix_round(acc[ti].y);
+                        if (ti == 4) { vx += fix_round(acc[9].x); vy += fix_round(acc[9].y); }
+                        atomicAdd(&dtp[0], (dt_t)vx);
+                        atomicAdd(&dtp[1], (dt_t)vy);
+                    }
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) dqa[u][i] += shfl2(dqa[u][i], o);
+            }
+            // every slice lane holds the sums: lane p < 4 stores member p
+            if (lane_ok && p < 4) {
+                f2 d[C / 2] = {dqa[0][0], dqa[0][1]};
+#pragma unroll
+                for (int u = 1; u < 4; ++u)
+                    if (p == u) { d[0] = dqa[u][0]; d[1] = dqa[u][1]; }
+                store_nat<C>(a.dq + token_info(g, w, tw).row * a.qs + coff, d, a.scale * ifs);
+            }
+        }
+
+        // ================= pass B: key quad -> dk, dv (rows staged above; no restage)
+        {
+            f2 kr[4][C / 2], vr[4][C / 2], dka[4][C / 2], dva[4][C / 2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = member(t0, u);
+                lds_row<C>(kr[u], kv_s + (size_t)t * 2 * C);
+                lds_row<C>(vr[u], kv_s + (size_t)t * 2 * C + C);
+#pragma unroll
+                for (int i = 0; i < C / 2; ++i) { dka[u][i] = splat(0.f); dva[u][i] = splat(0.f); }
+            }
+            const int ckoff = 2 * g.off - cq0;   // off - code(own member 0)
+#pragma unroll 1
+            for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nb); ++n) {
+                const int q0 = quad_tok(p + KS * n);
+                int2 mq[4];
+                mq[0] = meta_s[q0];
+                if (masked) {
+#pragma unroll
+                    for (int m = 1; m < 4; ++m) mq[m] = meta_s[member(q0, m)];
+                } else {
+                    mq[1] = mq[2] = mq[3] = mq[0];
+                }
+                const int tix0 = (mq[0].x & 0xffff) + ckoff;
+                f2 tb[9];
+                if (MMNI_PK4_TB9) {
+#pragma unroll
+                    for (int ti = 0; ti < 9; ++ti)
+                        lds_tab<1, NHP>(*reinterpret_cast<f2(*)[1]>(&tb[ti]), tab_s, tab_row(tix0, ti));
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    if (MMNI_PK4_SCHED) __builtin_amdgcn_sched_barrier(0);   // one query row in flight
+                    const int qt = member(q0, m);
+                    f2 ai[C / 2], gi[C / 2];
+                    lds_row<C>(ai, qg_s + (size_t)qt * 2 * C);
+                    lds_row<C>(gi, qg_s + (size_t)qt * 2 * C + C);
+                    const float4 x = *reinterpret_cast<const float4*>(rs_s + (size_t)qt * 2 * NH);
+                    const f2 ls = (f2){x.x, x.y}, nd = (f2){x.z, x.w};
+                    if (!MMNI_PK4_TB9) {
+#pragma unroll
+                        for (int kn = 0; kn < 4; ++kn) {
+                            const int ti = ((m & 1) - (kn & 1) + 1) * 3 + ((m >> 1) - (kn >> 1) + 1);
+                            lds_tab<1, NHP>(*reinterpret_cast<f2(*)[1]>(&tb[ti]), tab_s, tab_row(tix0, ti));
+                        }
+                    }
+#pragma unroll
+                    for (int kn = 0; kn < 4; ++kn) {
+                        const int ti = ((m & 1) - (kn & 1) + 1) * 3 + ((m >> 1) - (kn >> 1) + 1);
+                        f2 base = tb[ti] - ls;
+                        if (masked) base += splat(((mq[m].x >> 16) == rcq[kn] ? 0.f : kMask2) + __int_as_float(mq[m].y));
+                        f2 sc = pfma(ai[0], kr[kn][0], base);
+                        sc = pfma(ai[1], kr[kn][1], sc);
+                        const f2 pr = exp2_2(sc);
+                        f2 tt = pfma(gi[0], vr[kn][0], nd);
+                        tt = pfma(gi[1], vr[kn][1], tt);
+                        const f2 dsv = pr * tt;
+                        dva[kn][0] = pfma(pr, gi[0], dva[kn][0]);
+                        dva[kn][1] = pfma(pr, gi[1], dva[kn][1]);
+                        dka[kn][0] = pfma(dsv, ai[0], dka[kn][0]);
+                        dka[kn][1] = pfma(dsv, ai[1], dka[kn][1]);
+                    }
+                }
+            }
+            for (int o = 1; o < KS; o <<= 1) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int i = 0; i < C / 2; ++i) {
+                        dka[u][i] += shfl2(dka[u][i], o);
+                        dva[u][i] += shfl2(dva[u][i], o);
+                    }
+            }
+            if (lane_ok && p < 4) {
+                f2 dk[C / 2] = {dka[0][0], dka[0][1]}, dv[C / 2] = {dva[0][0], dva[0][1]};
+#pragma unroll
+                for (int u = 1; u < 4; ++u)
+                    if (p == u) { dk[0] = dka[u][0]; dk[1] = dka[u][1]; dv[0] = dva[u][0]; dv[1] = dva[u][1]; }
+                const int64_t rw = token_info(g, w, tw).row;
+                store_nat<C>(a.dv + rw * a.vs + coff, dv, ifs);
+                store_nat<C>(a.dk + rw * a.ks + coff, dk, kLn2 * ifs);
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
+        const dt_t v = dtab_s[(e / NH) * DS + e % NH];
+        if (v != 0) atomicAdd(&a.dtab_fix[(e / NH) * NHT + h0 + e % NH], v);
+    }
+}
+
 template <int C, int MAXT>
 static void* pk_fwd(int kind) {
     return kind ? reinterpret_cast<void*>(&wattn_fwd_pk_kernel<C, 1, MAXT>)
@@ -1239,10 +1534,11 @@ static void* pk2_fwd(int kind) {
 // gradient) allows one block per CU; it keeps 1024 threads (KS = 4) for occupancy.
 // qpl_f / qpl_b: rows per lane of the forward / backward (2: the pk2 kernels, windows of even N;
 // the two-row backward needs one window per block, N > 128).
-int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
+int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
                      int& qpl_b, int& hs_b, int& hs_f) {
     const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
-    const bool two_b = MMNI_BWD_QPL == 2 && kind == 0 && N % 2 == 0 && N > 128;
+    const bool two_b = MMNI_BWD_QPL >= 2 && kind == 0 && N % 2 == 0 && N > 128;
+    const bool four_b = two_b && MMNI_BWD_QPL == 4 && MMNI_BWD_HSPLIT == 3 && quad;
     qpl_f = two ? 2 : 1;
     qpl_b = 1;
     hs_b = 1;
@@ -1252,7 +1548,13 @@ int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, 
         kf = two ? (MMNI_FWD_HSPLIT == 3 ? pk2_fwd<4, 512>(kind) : pk2_fwd<12, 512>(kind)) : pk_fwd<12, 512>(kind);
         if (two) hs_f = MMNI_FWD_HSPLIT == 3 ? 3 : 1;
         maxt_f = 512;
-        if (two_b) {
+        if (four_b) {
+            // four rows per lane, one block per (window, head pair)
+            kb = reinterpret_cast<void*>(&wattn_bwd_pk4_kernel<4, 512>);
+            hs_b = 3;
+            maxt_b = 512;
+            qpl_b = 4;
+        } else if (two_b) {
             // MMNI_BWD_HSPLIT 3: one block per (window, head pair), 4 channels each
             kb = MMNI_BWD_HSPLIT == 3 ? reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<4, 512>)
                                       : reinterpret_cast<void*>(&wattn_bwd_pk2_kernel<12, 512>);
