@@ -22,6 +22,9 @@
 #ifndef MMNI_ABL
 #define MMNI_ABL 0
 #endif
+#ifndef MMNI_PK2_OPAQUE
+#define MMNI_PK2_OPAQUE 1   // two-row backward: row base opaque per window (no hoisted addresses)
+#endif
 
 namespace mmni {
 
@@ -891,7 +894,7 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
     const bool lane_ok = r < NHALF;
-    const int rr = lane_ok ? r : 0;
+    const int rr0 = lane_ok ? r : 0;
 
     for (int e = tid; e < g.Tsz * NHP; e += blockDim.x) {
         const int row = e / NHP, h = e - row * NHP;
@@ -906,6 +909,10 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
 
     for (int grp = wfirst; grp < a.ngroups; grp += gridDim.x / NHG) {
         const int w = grp;
+        // rr opaque per window (MMNI_PK2_OPAQUE): addresses derived from it are not hoisted out
+        // of the window loop, where they would stay live across both passes
+        int rr = rr0;
+        if (MMNI_PK2_OPAQUE) asm volatile("" : "+v"(rr));
         const bool active = lane_ok && (w < g.nwin);
         const bool masked = group_masked(g, grp, 1, NPAD);
         f2 aq[2][C / 2], dO[2][C / 2], lse2[2][NP], ndl[2][NP];
