@@ -612,21 +612,22 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
 
 // qpl: queries per lane (2 for wattn_fwd_pk2_kernel): a window occupies N / qpl x KS lanes.
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
-    const int chunk = packed ? (qpl == 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
+    const int chunk = packed ? (qpl >= 2 && !(bwd && qpl == 4) ? MMNI_PK2_CHUNK : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl == 4 ? 8 : qpl == 2 ? (bwd ? 4 : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    int KS = qpl >= 2 ? (bwd ? (qpl == 4 ? 8 : 4) : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (R * KS);
     if (qpl == 2 && !bwd && WPB > MMNI_PK2_FWD_WPB) WPB = MMNI_PK2_FWD_WPB;
+    if (qpl == 4 && !bwd && WPB > MMNI_PK4_FWD_WPB) WPB = MMNI_PK4_FWD_WPB;
     if (WPB < 1) WPB = 1;
     // the quad backward walks N / 4 bases per slice and stages exactly the window's rows
-    const int NPAD = qpl == 4 ? N : (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
+    const int NPAD = (bwd && qpl == 4) ? N : (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
     // the quad backward stages the scaled q / dO rows beside K / V (no restage between its passes)
-    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) + (qpl == 4 ? (size_t)NPAD * 2 * C * 4 : 0);
+    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) + (bwd && qpl == 4 ? (size_t)NPAD * 2 * C * 4 : 0);
     MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
     cfg.KS = KS;
     cfg.WPB = WPB;

@@ -90,13 +90,16 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #define MMNI_TAB_SWZ 1
 #endif
 #ifndef MMNI_FWD_QPL
-#define MMNI_FWD_QPL 2        // queries per lane of the packed C = 12 forward
+#define MMNI_FWD_QPL 2        // queries per lane of the packed C = 12 forward (4: head-pair blocks only)
 #endif
 #ifndef MMNI_PK2_CHUNK
 #define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
 #endif
 #ifndef MMNI_BWD_QPL
 #define MMNI_BWD_QPL 2        // rows per lane of the packed C = 12 backward (kind 0): 2, or 4 (quads; wd, wh even)
+#endif
+#ifndef MMNI_PK4_FWD_WPB
+#define MMNI_PK4_FWD_WPB 4    // windows per block of the four-query forward (MMNI_FWD_QPL 4)
 #endif
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward

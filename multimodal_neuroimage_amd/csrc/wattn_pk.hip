@@ -259,13 +259,13 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
 // broadcast ds_read_b128 costs the same LDS cycles as a scattered one.  Here each lane carries
 // queries t and t + N/2 of its window against the same keys, so every K/V/metadata read serves
 // two queries (LDS instructions per query-key pair 8.5 -> 5).  Lanes per window: N/2 x KS.
-template <int C, int KIND, int MAXT>
+template <int C, int KIND, int MAXT, int QPL = 2>
 __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
     constexpr int HD = 2, NH = C / HD, NP = NH / 2, CK = MMNI_PK2_CHUNK;
     static_assert(NH % 2 == 0, "head pairs");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WGeom& g = a.g;
-    const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB, NHALF = N / 2;
+    const int N = g.N, NPAD = a.NPAD, KS = a.KS, WPB = a.WPB, NHALF = N / QPL;   // QPL queries per lane: t, t + N/QPL, ...
     float* kv_s = smem;                                              // [WPB*NPAD][2C] pk k | pk v
     int2* meta_s = reinterpret_cast<int2*>(kv_s + (size_t)WPB * NPAD * 2 * C);  // [WPB*NPAD]
     float* tab_s = reinterpret_cast<float*>(meta_s + WPB * NPAD);     // [Tsz][NH]
@@ -319,11 +319,11 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
 
         const int w = grp * WPB + wl;
         const bool active = (wl < WPB) && (w < g.nwin);
-        f2 q[2][C / 2];
-        int cq[2] = {0, 0}, rq[2] = {0, 0};
-        int64_t row[2] = {0, 0};
+        f2 q[QPL][C / 2];
+        int cq[QPL] = {}, rq[QPL] = {};
+        int64_t row[QPL] = {};
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < QPL; ++u) {
             float qr[C];
             if (active) {
                 const TokenInfo ti = token_info(g, w, t + u * NHALF);
@@ -342,9 +342,9 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
         }
         __syncthreads();
 
-        f2 m[2][NP], l[2][NP], acc[2][C / 2];
+        f2 m[QPL][NP], l[QPL][NP], acc[QPL][C / 2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < QPL; ++u) {
 #pragma unroll
             for (int P = 0; P < NP; ++P) { m[u][P] = splat(-INFINITY); l[u][P] = splat(0.f); }
 #pragma unroll
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
         const int2* mw = meta_s + wl_c * NPAD;
         const int nk = NPAD / KS;
         for (int n = 0; n < nk; n += CK) {
-            f2 s[2][CK][NP];
+            f2 s[QPL][CK][NP];
 #pragma unroll
             for (int cc = 0; cc < CK; ++cc) {
                 const int j = p + KS * (n + cc);
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) kk[i] = kr[i];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < QPL; ++u) {
                     const float madd = (rcj == rq[u] ? 0.f : kMask2) + __int_as_float(mt.y);
                     const f2* tb = reinterpret_cast<const f2*>(tab_s + (cq[u] - code) * NH);
 #pragma unroll
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < QPL; ++u) {
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
                     f2 cm = s[u][0][P];
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) vv[i] = vr[i];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < QPL; ++u) {
 #pragma unroll
                     for (int P = 0; P < NP; ++P) {
                         const f2 pj = exp2_2(s[u][cc][P] - m[u][P]);
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
         }
         for (int o = 1; o < KS; o <<= 1) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < QPL; ++u) {
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
                     const f2 mo = shfl2(m[u][P], o), lo = shfl2(l[u][P], o);
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
         }
         if (active && p == 0) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < QPL; ++u) {
                 f2 op[C / 2];
 #pragma unroll
                 for (int P = 0; P < NP; ++P) {
@@ -1530,10 +1530,10 @@ static void* pk_bwd(int kind) {
                 : reinterpret_cast<void*>(&wattn_bwd_pk_kernel<C, 0, MAXT>);
 }
 
-template <int C, int MAXT>
+template <int C, int MAXT, int QPL = 2>
 static void* pk2_fwd(int kind) {
-    return kind ? reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 1, MAXT>)
-                : reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 0, MAXT>);
+    return kind ? reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 1, MAXT, QPL>)
+                : reinterpret_cast<void*>(&wattn_fwd_pk2_kernel<C, 0, MAXT, QPL>);
 }
 
 // Forward blocks of <= 512 threads (KS = 2 at N = 216): two blocks share a CU, so one block's
@@ -1543,7 +1543,9 @@ static void* pk2_fwd(int kind) {
 // the two-row backward needs one window per block, N > 128).
 int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
                      int& qpl_b, int& hs_b, int& hs_f) {
-    const bool two = MMNI_FWD_QPL == 2 && N % 2 == 0 && N >= 64;
+    const bool two = MMNI_FWD_QPL >= 2 && N % 2 == 0 && N >= 64;
+    // four queries per lane: head-pair blocks only (the C = 12 state of four rows does not fit)
+    const bool four = MMNI_FWD_QPL == 4 && MMNI_FWD_HSPLIT == 3 && N % 4 == 0 && N >= 64;
     const bool two_b = MMNI_BWD_QPL >= 2 && kind == 0 && N % 2 == 0 && N > 128;
     const bool four_b = two_b && MMNI_BWD_QPL == 4 && MMNI_BWD_HSPLIT == 3 && quad;
     qpl_f = two ? 2 : 1;
@@ -1552,8 +1554,10 @@ int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, in
     hs_f = 1;
     if (C == 12) {
         // MMNI_FWD_HSPLIT 3: the two-query forward per (window group, head pair)
-        kf = two ? (MMNI_FWD_HSPLIT == 3 ? pk2_fwd<4, 512>(kind) : pk2_fwd<12, 512>(kind)) : pk_fwd<12, 512>(kind);
+        kf = four ? pk2_fwd<4, 512, 4>(kind)
+                  : two ? (MMNI_FWD_HSPLIT == 3 ? pk2_fwd<4, 512>(kind) : pk2_fwd<12, 512>(kind)) : pk_fwd<12, 512>(kind);
         if (two) hs_f = MMNI_FWD_HSPLIT == 3 ? 3 : 1;
+        if (four) qpl_f = 4;
         maxt_f = 512;
         if (four_b) {
             // four rows per lane, one block per (window, head pair)
