@@ -148,6 +148,12 @@ __global__ __launch_bounds__(256) void conv3d_dx_kernel(ConvArgs a) {
 //   MODE 0 (forward):  out[v][o] = bias[o] + sum_t sum_i x[v + t - 1][i] * w[o][i][t], LeakyReLU
 //   MODE 1 (dx):       dx[v][i]  = sum_t sum_o dz[v + 1 - t][o] * w[o][i][t],
 //                      dz = dy * LeakyReLU'(y) computed once per halo row while staging.
+#ifndef MMNI_CONV_TAPW
+#define MMNI_CONV_TAPW 1   // k3 tile kernel: tap-inner loop with t-contiguous weight loads
+#endif
+#ifndef MMNI_CONV_TILE_ALL
+#define MMNI_CONV_TILE_ALL 1   // k3 forward: LDS tile for every channel pair (0: r05 selection)
+#endif
 constexpr int kTX = 8, kTY = 8, kTZ = 4;
 constexpr int kHX = kTX + 2, kHY = kTY + 2, kHZ = kTZ + 2;
 
@@ -202,6 +208,31 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
     float acc[NO];
 #pragma unroll
     for (int o = 0; o < NO; ++o) acc[o] = (MODE == 0 && a.bias) ? a.bias[o] : 0.f;
+#if MMNI_CONV_TAPW
+    // Tap-inner order: for one staged channel i, the 27 tap values come from LDS, and the weights of
+    // one (i, o) pair are 27 consecutive floats (PyTorch layout, t fastest), fetched with a few wide
+    // scalar loads.  The tap-outer order below issues one s_load_dword plus a 64-bit address add per
+    // weight (~6 SALU per VALU FMA pair at 24 -> 12: scalar-issue bound).
+    const float* hb = halo + ((tz * kHY + ty) * kHX + tx) * RS;
+#pragma unroll 1
+    for (int i = 0; i < NI; ++i) {
+        float xv[27];
+#pragma unroll
+        for (int t = 0; t < 27; ++t) {
+            const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
+            const int hz = MODE == 0 ? kz : 2 - kz, hy = MODE == 0 ? ky : 2 - ky, hx = MODE == 0 ? kx : 2 - kx;
+            xv[t] = hb[((hz * kHY + hy) * kHX + hx) * RS + i];
+        }
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const float* wp = a.w + (MODE == 0 ? (o * CIN + i) : (i * CIN + o)) * 27;
+            float sacc = acc[o];
+#pragma unroll
+            for (int t = 0; t < 27; ++t) sacc = fmaf(xv[t], wp[t], sacc);
+            acc[o] = sacc;
+        }
+    }
+#else
     for (int t = 0; t < 27; ++t) {
         const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
         // forward reads x[v + k - 1] = halo[v_local + k]; dx reads dz[v + 1 - k] = halo[v_local + 2 - k]
@@ -234,6 +265,7 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
             acc[o] = sacc;
         }
     }
+#endif
     const int gx = bx * kTX + tx, gy = by * kTY + ty, gz = bz * kTZ + tz;
     if (gx >= a.W || gy >= a.H || gz >= a.D) return;
     const int64_t vox = (((int64_t)b * a.D + gz) * a.H + gy) * a.W + gx;
@@ -377,7 +409,7 @@ template <int CIN, int COUT>
 static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
     // measured at 96^3 (r05): the LDS tile wins for CIN <= 12 with >= 6 outputs, or CIN <= 3; the
     // lane-per-voxel gather is faster for 24 -> 12 (tile LDS 67 KB: 2 blocks/CU) and 6 -> 3
-    if (is_k3_same(a) && ((CIN <= 12 && COUT >= 6) || CIN <= 3)) {
+    if (is_k3_same(a) && (MMNI_CONV_TILE_ALL || (CIN <= 12 && COUT >= 6) || CIN <= 3)) {
         conv3d_k3_tile_kernel<CIN, COUT, 0><<<k3_tiles(a), 256, 0, s>>>(a);
         return launch_status("conv3d_fwd_k3");
     }
