@@ -295,17 +295,26 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
     float* x_s = dz_s + Tout * COUT;          // [Tin][CIN]
     const int tid = threadIdx.x;
     float acc[MAXP][COUT];
-    float dbacc[COUT];
+    float dbs = 0.f;   // db[pl] partial (lanes pl < COUT)
 #pragma unroll
     for (int m = 0; m < MAXP; ++m)
 #pragma unroll
         for (int co = 0; co < COUT; ++co) acc[m][co] = 0.f;
-#pragma unroll
-    for (int co = 0; co < COUT; ++co) dbacc[co] = 0.f;
     const int tiles_per_b = a.ntz * a.nty * a.ntx;
     const int G = MAXP == 1 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;   // lane groups over voxels
     const int gi = MAXP == 1 ? tid / npairs : 0;
     const int pl = MAXP == 1 ? tid - gi * npairs : tid;
+    const int plc = pl < COUT ? pl : COUT - 1;
+    // x_s offset of each owned pair relative to the voxel's halo base
+    int xo[MAXP];
+#pragma unroll
+    for (int m = 0; m < MAXP; ++m) {
+        const int p = pl + m * 256;
+        const int pv = p < npairs ? p : 0;
+        const int ci = pv % CIN, t = pv / CIN;
+        const int tx = t % a.kw, ty = (t / a.kw) % a.kh, tz = t / (a.kw * a.kh);
+        xo[m] = ((tz * a.HY + ty) * a.HX + tx) * CIN + ci;
+    }
 
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         int rr = tile;
@@ -346,28 +355,26 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
         }
         __syncthreads();
         // pair (t, ci) owned by this lane: p = tid + m*256; with fewer pairs than lanes (MAXP 1)
-        // the block splits into G groups of npairs lanes that take every G-th output voxel
+        // the block splits into G groups of npairs lanes that take every G-th output voxel.
+        // Lanes past the last pair (or group) compute on pair 0 and are dropped at the flush, so
+        // the loop has no per-pair branch; the voxel coordinates advance without divisions.
+        int ux = gi % a.TX, uy = (gi / a.TX) % a.TY, uz = gi / (a.TX * a.TY);
         for (int u = gi; u < Tout; u += G) {
-            const int ux = u % a.TX, uy = (u / a.TX) % a.TY, uz = u / (a.TX * a.TY);
+            const int hb = ((uz * a.sd * a.HY) + uy * a.sh) * a.HX + ux * a.sw;
             float g[COUT];
 #pragma unroll
             for (int co = 0; co < COUT; ++co) g[co] = dz_s[u * COUT + co];
-            if (pl < COUT && gi < G) {
-#pragma unroll
-                for (int co = 0; co < COUT; ++co)
-                    if (co == pl) dbacc[co] += g[co];
-            }
+            dbs += dz_s[u * COUT + plc];
 #pragma unroll
             for (int m = 0; m < MAXP; ++m) {
-                const int p = pl + m * 256;
-                if (p < npairs && gi < G) {
-                    const int ci = p % CIN, t = p / CIN;
-                    const int tx = t % a.kw, ty = (t / a.kw) % a.kh, tz = t / (a.kw * a.kh);
-                    const int hv = ((uz * a.sd + tz) * a.HY + (uy * a.sh + ty)) * a.HX + (ux * a.sw + tx);
-                    const float xv = x_s[hv * CIN + ci];
+                const float xv = x_s[hb * CIN + xo[m]];
 #pragma unroll
-                    for (int co = 0; co < COUT; ++co) acc[m][co] = fmaf(g[co], xv, acc[m][co]);
-                }
+                for (int co = 0; co < COUT; ++co) acc[m][co] = fmaf(g[co], xv, acc[m][co]);
+            }
+            ux += G;
+            while (ux >= a.TX) {
+                ux -= a.TX;
+                if (++uy == a.TY) { uy = 0; ++uz; }
             }
         }
     }
@@ -380,11 +387,7 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             for (int co = 0; co < COUT; ++co) atomicAdd(&a.dw[((int64_t)co * CIN + ci) * K3 + t], acc[m][co]);
         }
     }
-    if (a.db && pl < COUT && gi < G) {
-#pragma unroll
-        for (int co = 0; co < COUT; ++co)
-            if (co == pl) atomicAdd(&a.db[co], dbacc[co]);
-    }
+    if (a.db && pl < COUT && gi < G) atomicAdd(&a.db[pl], dbs);
 }
 
 static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
