@@ -22,6 +22,9 @@
 #ifndef MMNI_ABL
 #define MMNI_ABL 0
 #endif
+#ifndef MMNI_PK2_PAIRQ
+#define MMNI_PK2_PAIRQ 0   // two-row backward pass B: queries i and i + N/2 together (3 table reads per 4 pairs; measured slower)
+#endif
 #ifndef MMNI_PK2_OPAQUE
 #define MMNI_PK2_OPAQUE 1   // two-row backward: row base opaque per window (no hoisted addresses)
 #endif
@@ -1149,11 +1152,9 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
 #pragma unroll
                 for (int i = 0; i < C / 2; ++i) { dka[u][i] = splat(0.f); dva[u][i] = splat(0.f); }
             const int ck0 = g.off - code[0], ck1 = g.off - code[1];
-            const int ib = p * nk;
-            for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nk); ++n) {
-                const int i = ib + n;
-                const int2 mcur = meta_s[i];
-                const int ci = mcur.x & 0xffff, ri = mcur.x >> 16;
+            // one query row i against the lane's two keys, with their table rows
+            auto qrow = [&](int i, int2 mcur, const f2 (&tb0)[NP], const f2 (&tb1)[NP]) {
+                const int ri = mcur.x >> 16;
                 f2 ai[C / 2], gi[C / 2];
                 lds_row<C>(ai, rowb + (size_t)i * 2 * C);
                 lds_row<C>(gi, rowb + (size_t)i * 2 * C + C);
@@ -1169,9 +1170,7 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
                 }
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
-                    const int tix = ci + (u ? ck1 : ck0);
-                    f2 tb[NP];
-                    lds_tab<NP, NHP>(tb, tab_s, tix);
+                    const f2(&tb)[NP] = u ? tb1 : tb0;
                     f2 base[NP];
                     if (masked) {
                         const float madd = (ri == rc[u] ? 0.f : kMask2) + __int_as_float(mcur.y);
@@ -1194,6 +1193,35 @@ __global__ __launch_bounds__(MAXT, C == 4 ? 4 : 1) void wattn_bwd_pk2_kernel(WAA
                         dka[u][2 * P] = pfma(dsv, ai[2 * P], dka[u][2 * P]);
                         dka[u][2 * P + 1] = pfma(dsv, ai[2 * P + 1], dka[u][2 * P + 1]);
                     }
+                }
+            };
+            // Paired queries (as pass A's paired keys): query i + N/2 against key rr + N/2 has the
+            // table row of query i against key rr, so queries i and i + N/2 together take 3 table
+            // reads for their 4 pairs instead of 4.
+            const bool pairedB = MMNI_PK2_PAIRQ && NPAD == N && NHALF % (g.wh * g.ww) == 0 && NHALF % KS == 0;
+            if (pairedB) {
+                const int nk2 = NHALF / KS, ib2 = p * nk2;
+                for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nk2); ++n) {
+                    const int i0 = ib2 + n, i1 = i0 + NHALF;
+                    const int2 m0 = meta_s[i0], m1 = meta_s[i1];
+                    const int c0 = m0.x & 0xffff;
+                    f2 tA[NP], tB[NP], tC[NP];
+                    lds_tab<NP, NHP>(tA, tab_s, c0 + ck0);                 // (i0, rr), (i1, rr + N/2)
+                    lds_tab<NP, NHP>(tB, tab_s, c0 + ck1);                 // (i0, rr + N/2)
+                    lds_tab<NP, NHP>(tC, tab_s, (m1.x & 0xffff) + ck0);    // (i1, rr)
+                    qrow(i0, m0, tA, tB);
+                    qrow(i1, m1, tC, tA);
+                }
+            } else {
+                const int ib = p * nk;
+                for (int n = 0; n < ((MMNI_ABL & 2) ? 0 : nk); ++n) {
+                    const int i = ib + n;
+                    const int2 mcur = meta_s[i];
+                    const int ci = mcur.x & 0xffff;
+                    f2 tb0[NP], tb1[NP];
+                    lds_tab<NP, NHP>(tb0, tab_s, ci + ck0);
+                    lds_tab<NP, NHP>(tb1, tab_s, ci + ck1);
+                    qrow(i, mcur, tb0, tb1);
                 }
             }
             for (int o = 1; o < KS; o <<= 1) {
