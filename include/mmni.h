@@ -147,7 +147,8 @@ typedef struct mmni_conv3d_desc {
     float   slope;              /* fused LeakyReLU negative slope; 1.0 = identity         */
 } mmni_conv3d_desc;
 
-/* Input is read as (B, D, H, W, Cin) channels-last; output written (B, Do, Ho, Wo, Cout). */
+/* Input is read as (B, D, H, W, Cin) channels-last; output written (B, Do, Ho, Wo, Cout).
+   w is (Cout, Cin, kd, kh, kw) contiguous; 8-byte aligned for the k3 s1 p1 case (< 0 otherwise). */
 int mmni_conv3d_fwd(const mmni_conv3d_desc* d, const float* x, const float* w,
                     const float* bias, float* y, void* stream);
 /* dx overwritten (may be NULL); dw (Cout*Cin*kd*kh*kw) and db (Cout) ACCUMULATED (caller zeroes).

@@ -452,6 +452,7 @@ static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
     // measured at 96^3 (r05): the LDS tile wins for CIN <= 12 with >= 6 outputs, or CIN <= 3; the
     // lane-per-voxel gather is faster for 24 -> 12 (tile LDS 67 KB: 2 blocks/CU) and 6 -> 3
     if (is_k3_same(a) && (MMNI_CONV_TILE_ALL || (CIN <= 12 && COUT >= 6) || CIN <= 3)) {
+        MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(a.w) % 8 == 0, "conv3d_fwd: k3 weights must be 8-byte aligned");
         conv3d_k3_tile_kernel<CIN, COUT, 0><<<k3_tiles(a), 256, 0, s>>>(a);
         return launch_status("conv3d_fwd_k3");
     }
