@@ -157,6 +157,9 @@ __global__ __launch_bounds__(256) void conv3d_dx_kernel(ConvArgs a) {
 #ifndef MMNI_CONV_PAIRW_SB
 #define MMNI_CONV_PAIRW_SB 1
 #endif
+#ifndef MMNI_CONV_DW_BPC
+#define MMNI_CONV_DW_BPC 8   // dW kernel: persistent blocks per CU (each flushes its partials once)
+#endif
 #ifndef MMNI_CONV_TILE_ALL
 #define MMNI_CONV_TILE_ALL 1   // k3 forward: LDS tile for every channel pair (0: r05 selection)
 #endif
@@ -417,16 +420,44 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             }
         }
     }
+    // lane groups (MAXP 1, G > 1): sum the G partials of a pair through LDS first, so a block
+    // flushes one atomic per (pair, co) rather than G (same-address atomics serialise in L2)
+    bool flush = gi < G;
+    if (MAXP == 1 && G > 1) {
+        __syncthreads();
+        float* red = smem;                        // [G][npairs][COUT], then [G][COUT] db partials
+        float* redb = red + G * npairs * COUT;
+        if (gi < G) {
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) red[(gi * npairs + pl) * COUT + co] = acc[0][co];
+            if (pl < COUT) redb[gi * COUT + pl] = dbs;
+        }
+        __syncthreads();
+        if (gi == 0) {
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) {
+                float sum = 0.f;
+                for (int q = 0; q < G; ++q) sum += red[(q * npairs + pl) * COUT + co];
+                acc[0][co] = sum;
+            }
+            if (pl < COUT) {
+                float sum = 0.f;
+                for (int q = 0; q < G; ++q) sum += redb[q * COUT + pl];
+                dbs = sum;
+            }
+        }
+        flush = gi == 0;
+    }
 #pragma unroll
     for (int m = 0; m < MAXP; ++m) {
         const int p = pl + m * 256;
-        if (p < npairs && gi < G) {
+        if (p < npairs && flush) {
             const int ci = p % CIN, t = p / CIN;
 #pragma unroll
             for (int co = 0; co < COUT; ++co) atomicAdd(&a.dw[((int64_t)co * CIN + ci) * K3 + t], acc[m][co]);
         }
     }
-    if (a.db && pl < COUT && gi < G) atomicAdd(&a.db[pl], dbs);
+    if (a.db && pl < COUT && flush) atomicAdd(&a.db[pl], dbs);
 }
 
 static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
@@ -495,8 +526,12 @@ static int conv_bwd_launch(ConvArgs& a, hipStream_t s) {
     a.ntz = (a.Do + TZ - 1) / TZ; a.nty = (a.Ho + TY - 1) / TY; a.ntx = (a.Wo + TX - 1) / TX;
     a.ntiles = a.B * a.ntz * a.nty * a.ntx;
     const int npairs = a.kd * a.kh * a.kw * CIN;
-    int grid = a.ntiles < kNumCU * 4 ? a.ntiles : kNumCU * 4;
-    const size_t lds = bytes();
+    int grid = a.ntiles < kNumCU * MMNI_CONV_DW_BPC ? a.ntiles : kNumCU * MMNI_CONV_DW_BPC;
+    // the group reduction of the MAXP 1 kernel reuses the LDS image: [G][npairs][COUT] + [G][COUT]
+    const int G = npairs <= 256 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;
+    const size_t red = (size_t)G * (npairs + 1) * COUT * 4;
+    const size_t lds = bytes() > red ? bytes() : red;
+    MMNI_ARG_CHECK(lds <= 64 * 1024, "conv3d_dw: group reduction exceeds the LDS tile");
 #define MMNI_DW(MP)                                                                            \
     conv3d_dw_kernel<CIN, COUT, MP><<<grid, 256, lds, s>>>(a);                                 \
     return launch_status("conv3d_dw");
