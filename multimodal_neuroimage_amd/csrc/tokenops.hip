@@ -125,6 +125,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t rows, const 
 //            double result is split into hi + lo floats stored IN PLACE in the slice's first two
 //            rows (same column: no other block reads them);
 //   stage 2  one lane per column adds the slices' (hi + lo) in slice order, in double.
+constexpr int kColSlices = 16;   // row slices of stage 1 (stage 2 holds one value pair per slice)
+
 template <int CW>
 __global__ __launch_bounds__(1024) void column_sum_stage1_kernel(float* __restrict__ part, int nparts, int ncols,
                                                                  int rps) {
@@ -159,11 +161,21 @@ __global__ __launch_bounds__(256) void column_sum_stage2_kernel(const float* __r
                                                                 int split, float* __restrict__ out2) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= ncols) return;
-    double t = 0.0;
-    for (int sl = 0; sl < nslices; ++sl) {
+    // all slice loads issued before the (in-order, double) sum: one memory latency, not 2 x nslices
+    float hi[kColSlices], lo[kColSlices];
+#pragma unroll
+    for (int sl = 0; sl < kColSlices; ++sl) {
         const int r0 = sl * rps;
-        t += (double)part[(int64_t)r0 * ncols + j];
-        if (nparts - r0 > 1) t += (double)part[(int64_t)(r0 + 1) * ncols + j];
+        hi[sl] = sl < nslices ? part[(int64_t)r0 * ncols + j] : 0.f;
+        lo[sl] = (sl < nslices && nparts - r0 > 1) ? part[(int64_t)(r0 + 1) * ncols + j] : 0.f;
+    }
+    double t = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < kColSlices; ++sl) {
+        if (sl < nslices) {
+            t += (double)hi[sl];
+            if (nparts - sl * rps > 1) t += (double)lo[sl];
+        }
     }
     if (j < split) out[j] = (float)t;
     else if (out2) out2[j - split] = (float)t;
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(256) void column_sum_stage2_kernel(const float* __r
 
 void column_sum(const float* part_c, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
     float* part = const_cast<float*>(part_c);   // scratch: stage 1 leaves its sums in place
-    const int want = 16;                        // row slices
+    const int want = kColSlices;                // row slices
     int rps = (nparts + want - 1) / want;
     if (rps < 2) rps = 2;
     const int nslices = (nparts + rps - 1) / rps;
