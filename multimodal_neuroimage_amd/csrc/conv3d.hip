@@ -386,7 +386,22 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
 #pragma unroll
             for (int co = 0; co < COUT; ++co) dz_s[e * COUT + co] = g[co];
         }
-        for (int e = tid; e < Tin * CIN; e += blockDim.x) {
+        // halo rows as float4 chunks when rows are 16-B multiples: the index math runs per chunk
+        const bool vec4 = CIN % 4 == 0 && (Tout * COUT) % 4 == 0 && reinterpret_cast<uintptr_t>(a.x) % 16 == 0;
+        if (vec4) {
+            constexpr int C4 = CIN / 4 > 0 ? CIN / 4 : 1;
+            for (int e = tid; e < Tin * C4; e += blockDim.x) {
+                const int c4 = e % C4, v = e / C4;
+                const int lx = v % a.HX, ly = (v / a.HX) % a.HY, lz = v / (a.HX * a.HY);
+                const int z = iz0 + lz, y = iy0 + ly, x = ix0 + lx;
+                float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (z >= 0 && z < a.D && y >= 0 && y < a.H && x >= 0 && x < a.W)
+                    xv = *reinterpret_cast<const float4*>(a.x + ((((int64_t)b * a.D + z) * a.H + y) * a.W + x) * CIN +
+                                                          4 * c4);
+                *reinterpret_cast<float4*>(x_s + v * CIN + 4 * c4) = xv;
+            }
+        }
+        for (int e = tid; e < (vec4 ? 0 : Tin * CIN); e += blockDim.x) {
             const int ci = e % CIN, v = e / CIN;
             const int lx = v % a.HX, ly = (v / a.HX) % a.HY, lz = v / (a.HX * a.HY);
             const int z = iz0 + lz, y = iy0 + ly, x = ix0 + lx;
