@@ -195,8 +195,17 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
         float v[NI];
         const bool in = gx >= 0 && gx < a.W && gy >= 0 && gy < a.H && gz >= 0 && gz < a.D;
         const int64_t row = in ? (((int64_t)b * a.D + gz) * a.H + gy) * a.W + gx : 0;
+        if (NI % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            // 16-B rows: float4 loads (NI / 4 per row instead of NI)
 #pragma unroll
-        for (int c = 0; c < NI; ++c) v[c] = in ? src[row * NI + c] : 0.f;
+            for (int c = 0; c < (NI % 4 == 0 ? NI : 0); c += 4) {
+                const float4 q = in ? *reinterpret_cast<const float4*>(src + row * NI + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[c] = q.x; v[c + 1] = q.y; v[c + 2] = q.z; v[c + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NI; ++c) v[c] = in ? src[row * NI + c] : 0.f;
+        }
         if (MODE == 1 && in && a.slope != 1.f) {
 #pragma unroll
             for (int c = 0; c < NI; ++c) v[c] *= lrelu_grad(a.y[row * NI + c], a.slope);
