@@ -1,7 +1,13 @@
 """Throughput benchmark of the MI355X hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4] [--batch B] [--size S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--batch B] [--size S]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+`--gpus N` with N > 1 outside a torch.distributed.run launch re-launches this script as N ranks
+(torch.distributed.run, one process per GPU, RCCL) from a parent that never touches the GPU, and
+exits with their status.  Inside a launch, WORLD_SIZE must equal --gpus; n_gpus in the JSON line
+is the process group's size.  `--dry-run` runs the same launcher / rank / timing plumbing on CPU
+(gloo) with a stand-in model, for the CPU tests.
 
 Workload (default): two-modality SwinFusion in the build's 3D lift on synthetic
 z-scored 96^3 sMRI+fMRI volume pairs, 4 pairs per GPU (weak scaling), fp32.  One step =
@@ -21,6 +27,8 @@ import glob
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,17 +38,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "volume-pairs/sec fwd+bwd, 96³ 2-modality batch, 1/2/4/8 MI355X"
+METRIC_C2 = "volumes/sec fwd+bwd, 96³ single-modality Swin-V2 (C2), 1/2/4/8 MI355X"
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 matrix dense peak
 HBM_PEAK_GBS = 8000.0
+
+# which roof bounds each HIP kernel family: "valu" = the fp32 compute roof on the
+# vector ALUs (the window attention at head_dim 2/4 issues no MFMA), "mfma" = the f32 matrix
+# cores, "hbm" = bandwidth (8 TB/s).
+BOUNDS = (("wattn_", "valu"), ("conv3d_fwd_1x", "hbm"), ("conv3d_bwd_1x", "hbm"), ("conv3d_", "valu"),
+          ("mha_", "mfma"), ("mlp_", "mfma"), ("ln_mlp_", "mfma"), ("ln_linear_", "mfma"), ("linear_bwd_", "mfma"),
+          ("layernorm_", "hbm"), ("token_linear_", "hbm"), ("linear_dw_", "hbm"))
+
+
+def kernel_bound(name):
+    for pre, b in BOUNDS:
+        if name.startswith(pre):
+            return b
+    return "hbm"
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=["c3", "c4"],
-                    help="c3: SwinFusion 3D (default, the BASELINE metric's config); c4: SwinCrossmodal3D composite")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"],
+                    help="c3: SwinFusion 3D (default, the BASELINE metric's config); c2: single-modality Swin-V2 "
+                         "3D; c4: SwinCrossmodal3D composite")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU (gloo) run of the launcher / rank / timing plumbing with a stand-in model")
     ap.add_argument("--batch", type=int, default=4, help="volume pairs per GPU")
     ap.add_argument("--size", type=int, default=96, help="volume side (voxels)")
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
@@ -94,13 +121,20 @@ def latest_pmc(kernel_name):
     return None, None
 
 
+def _cpu_threads():
+    """Host threads for the CPU baseline: the GPU box gives one GPU's job a 16-CPU share even though
+    os.cpu_count() reports the whole machine, so at most 16 (reported next to os.cpu_count())."""
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    return threads
+
+
 def cpu_baseline_c4(size):
     """Oracle composite (fp32 CPU) fwd+bwd on one pair at the full size: the crossmodal head's cost
     does not scale with a smaller volume in a simple way, so no sampling."""
     from multimodal_neuroimage_amd import model as M
     from oracle import model as OM   # cpu_baseline leg: the oracle is the timed CPU port
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads = _cpu_threads()
     m = M.SwinCrossmodal3D(**c4_kwargs(size))
     p = OM.params_of(m, torch.float32)
     g = torch.Generator().manual_seed(0)
@@ -111,18 +145,35 @@ def cpu_baseline_c4(size):
     out = OM.swin_crossmodal_logits(p, A, B, cfg)
     torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out)).backward()
     t = time.perf_counter() - t0
-    return dict(value=round(1.0 / t, 6), unit="volume-pairs/s", cores=threads, kind="port",
+    return dict(value=round(1.0 / t, 6), unit="volume-pairs/s", cores=threads, host_cpus=os.cpu_count(),
+                kind="port", extrapolated=False,
                 sample=f"oracle SwinCrossmodal3D fwd+bwd, 1 pair at {size}^3 ({t:.1f} s); fp32")
+
+
+def cpu_baseline_c2(size):
+    """Oracle single-modality Swin-V2 (fp32 CPU) fwd+bwd on one full-size volume (no sampling)."""
+    from multimodal_neuroimage_amd import model as M
+    from oracle import model as OM   # cpu_baseline leg: the oracle is the timed CPU port
+    threads = _cpu_threads()
+    m = M.SwinTransformerV2(**model_kwargs(size))
+    p = OM.params_of(m, torch.float32)
+    z = torch.randn(2, size, size, size, generator=torch.Generator().manual_seed(0))
+    t0 = time.perf_counter()
+    out = OM.swin_v2_logits(p, "", z, 8, 6)
+    torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out)).backward()
+    t = time.perf_counter() - t0
+    return dict(value=round(2.0 / t, 6), unit="volumes/s", cores=threads, host_cpus=os.cpu_count(), kind="port",
+                extrapolated=False, sample=f"oracle Swin-V2 3D fwd+bwd, 2 volumes at {size}^3 ({t:.1f} s); fp32")
 
 
 def cpu_baseline(size, sample):
     """Oracle (functional torch-CPU restatement) SwinFusion-3D fwd+bwd, bounded sample: the trunk
-    (conv + 60 window-attention blocks, cost linear in voxels) on one sample^3 pair scaled by the
-    voxel ratio, plus the Swin-V2 head at the full size^3 input (its cost does not scale)."""
+    (conv + 60 window-attention blocks, cost linear in voxels) on one sample^3 pair EXTRAPOLATED by
+    the voxel ratio, plus the Swin-V2 head at the full size^3 input (its cost does not scale).  A
+    full 96^3 pair would take ~20 CPU-minutes, beyond the bench's bounded budget."""
     from multimodal_neuroimage_amd import model as M
     from oracle import model as OM   # cpu_baseline leg: the oracle is the timed CPU port
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads = _cpu_threads()
     m = M.SwinFusion(**model_kwargs(size))
     p = OM.params_of(m, torch.float32)
     cfg = dict(window_size=6, Ex_depths=[6, 6], Fusion_depths=[2, 2, 2], Re_depths=[6, 6], heads=6,
@@ -140,16 +191,86 @@ def cpu_baseline(size, sample):
     t_head = time.perf_counter() - t0
     scale = (size / sample) ** 3
     t_pair = t_trunk * scale + t_head
-    return dict(value=round(1.0 / t_pair, 6), unit="volume-pairs/s", cores=threads, kind="port",
-                sample=f"oracle SwinFusion-3D fwd+bwd: trunk on 1 pair at {sample}^3 ({t_trunk:.1f} s, scaled "
-                       f"x{scale:.0f} by voxel count) + Swin-V2 head at {size}^3 ({t_head:.1f} s); fp32")
+    return dict(value=round(1.0 / t_pair, 6), unit="volume-pairs/s", cores=threads, host_cpus=os.cpu_count(),
+                kind="port", extrapolated=True,
+                sample=f"oracle SwinFusion-3D fwd+bwd: trunk timed on 1 pair at {sample}^3 ({t_trunk:.1f} s) and "
+                       f"extrapolated x{scale:.0f} by voxel count, + Swin-V2 head at {size}^3 ({t_head:.1f} s); fp32")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """Parent side of `--gpus N`: start N ranks with torch.distributed.run (one process per GPU,
+    rendezvous on 127.0.0.1) and return their exit status.  Runs before anything touches the GPU;
+    the ranks are child processes, never an exec of this one.  None when no launch is needed."""
+    n = args.gpus or 1
+    if "WORLD_SIZE" in os.environ or n <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, env, D):
+    """--dry-run: the bench's rank plumbing on CPU (gloo): DDP-wrapped stand-in, barrier-bracketed
+    timed steps, max over ranks, rank 0's JSON line with n_gpus from the process group."""
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    torch.manual_seed(0)
+    model = D.wrap_ddp(torch.nn.Sequential(torch.nn.Linear(12, 48), torch.nn.GELU(), torch.nn.Linear(48, 1)), env)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    x = torch.randn(args.batch, 12, generator=torch.Generator().manual_seed(env.rank))
+    y = torch.ones(args.batch, 1)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        torch.nn.functional.binary_cross_entropy_with_logits(model(x), y).backward()
+        opt.step()
+    for _ in range(args.warmup):
+        step()
+    D.barrier(env)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    D.barrier(env)
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, env)
+    grads = [p.grad.clone() for p in model.parameters()]
+    if env.enabled:   # gradients identical on every rank after the all-reduce
+        for g in grads:
+            ref = g.clone()
+            dist.broadcast(ref, 0)
+            assert torch.equal(ref, g)
+    if env.rank == 0:
+        print(json.dumps(dict(metric=METRIC, value=args.batch * world * args.steps / elapsed, unit="volume-pairs/s",
+                              n_gpus=world, steps=args.steps, warmup=args.warmup, dry_run=True,
+                              ms_per_step=elapsed / args.steps * 1e3, scaling="weak",
+                              config=dict(workload="dry run (CPU stand-in)", global_batch=args.batch * world,
+                                          parallelism=f"dp{world}"))), flush=True)
+    D.shutdown(env)
 
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     from multimodal_neuroimage_amd import distributed as D
-    env = D.init_from_env()            # one process per GPU, RCCL ("nccl") when WORLD_SIZE > 1
-    world, rank, device = env.world, env.rank, env.device
+    # one process per GPU, RCCL ("nccl") when WORLD_SIZE > 1 (gloo on CPU for --dry-run)
+    env = D.init_from_env(backend="gloo" if args.dry_run else None, use_cuda=not args.dry_run)
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launch has WORLD_SIZE {world}")
+    if args.dry_run:
+        return dry_run(args, env, D)
+    rank, device = env.rank, env.device
     torch.manual_seed(55555555)
 
     from multimodal_neuroimage_amd import model as M
@@ -157,17 +278,21 @@ def main():
 
     if args.config == "c4":
         model = D.wrap_ddp(M.SwinCrossmodal3D(use_checkpoint=args.checkpoint, **c4_kwargs(args.size)).to(device), env)
+    elif args.config == "c2":
+        model = D.wrap_ddp(M.SwinTransformerV2(use_checkpoint=args.checkpoint, **model_kwargs(args.size)).to(device),
+                           env)
     else:
         kw = model_kwargs(args.size)
         model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
     graph = args.graph and world == 1
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank)
+    inputs = (A,) if args.config == "c2" else (A, B)
     lossf = torch.nn.BCEWithLogitsLoss()
 
     def eager_step():
         opt.zero_grad(set_to_none=True)
-        out = model(A, B)["binary_classification"]
+        out = model(*inputs)["binary_classification"]
         loss = lossf(out, y)
         loss.backward()
         opt.step()
@@ -187,7 +312,7 @@ def main():
         g = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(g):
-            static_loss = lossf(model(A, B)["binary_classification"], y)
+            static_loss = lossf(model(*inputs)["binary_classification"], y)
             static_loss.backward()
             opt.step()
 
@@ -230,36 +355,52 @@ def main():
         dom_name, dom = max(kern.items(), key=lambda kv: kv[1]["total_ms"]) if kern else (None, None)
         roofline = None
         if dom is not None:
-            tflops = dom["flops_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e12
+            bound = kernel_bound(dom_name)
             traffic, pmc_file = latest_pmc(dom_name)
-            roofline = dict(kernel=dom_name, bound="mfma", achieved=round(tflops, 3), peak=FP32_PEAK_TFLOPS,
-                            unit="TFLOP/s", frac=round(tflops / FP32_PEAK_TFLOPS, 4), traffic=traffic,
+            tflops = dom["flops_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e12
+            gbs = dom["bytes_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e9
+            if bound == "hbm":
+                achieved, peak, unit = gbs, HBM_PEAK_GBS, "GB/s"
+            else:
+                achieved, peak, unit = tflops, FP32_PEAK_TFLOPS, "TFLOP/s"
+            notes = {"valu": "fp32 compute roof on the vector ALUs (157.3 TF, = the f32 MFMA rate); window "
+                             "attention at head_dim 2/4 has no MFMA-shaped contraction and issues no MFMA",
+                     "mfma": "f32 matrix-core roof (157.3 TF dense)",
+                     "hbm": "HBM3E bandwidth roof (8 TB/s)"}
+            roofline = dict(kernel=dom_name, bound=bound, achieved=round(achieved, 3), peak=peak, unit=unit,
+                            frac=round(achieved / peak, 4), traffic=traffic,
                             avg_ms=round(dom["avg_ms"], 4), launches_per_step=dom["launches"] / steps_timed,
                             share_of_step=round(dom["total_ms"] / steps_timed / ms, 3),
-                            algorithmic_bytes=dom["bytes_per_launch"],
-                            algorithmic_gbs=round(dom["bytes_per_launch"] / (dom["avg_ms"] * 1e-3) / 1e9, 1),
-                            note="fp32 compute roof (VALU = f32 MFMA rate); head_dim 2 leaves no MFMA-shaped "
-                                 "contraction; traffic from " + (pmc_file or "no PMC summary yet"))
+                            algorithmic_flops=dom["flops_per_launch"], algorithmic_bytes=dom["bytes_per_launch"],
+                            algorithmic_gbs=round(gbs, 1), algorithmic_tflops=round(tflops, 3),
+                            note=notes[bound] + "; traffic (HBM bytes per launch, PMC) from " +
+                            (pmc_file or "no PMC summary yet"))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline_c4(args.size) if args.config == "c4" else cpu_baseline(args.size,
-                                                                                          args.cpu_sample_size)
+                if args.config == "c4":
+                    cpu = cpu_baseline_c4(args.size)
+                elif args.config == "c2":
+                    cpu = cpu_baseline_c2(args.size)
+                else:
+                    cpu = cpu_baseline(args.size, args.cpu_sample_size)
             except Exception as e:  # the baseline is reported, never required
                 cpu = dict(error=str(e))
-        line = dict(metric=METRIC, value=round(value, 4), unit="volume-pairs/s", n_gpus=world, steps=args.steps,
+        workloads = {
+            "c3": dict(workload=f"C3: SwinFusion 3D lift, {args.size}^3 sMRI+fMRI pairs", patch=8, window=6,
+                       tokens_per_volume=args.size ** 3),
+            "c2": dict(workload=f"C2: single-modality Swin-V2 3D, {args.size}^3 volumes", patch=8, window=6,
+                       tokens_per_volume=(args.size // 8) ** 3),
+            "c4": dict(workload=f"C4: SwinCrossmodal3D composite, {args.size}^3 pairs, crossmodal head "
+                                f"12 layers x 12 heads on {(args.size // 8) ** 3}-token sequences",
+                       patch=8, window=6, sequence=(args.size // 8) ** 3)}
+        config = dict(workloads[args.config], global_batch=args.batch * world, per_gpu_batch=args.batch,
+                      volume=args.size, parallelism=f"dp{world}", checkpoint=args.checkpoint, graph=graph)
+        line = dict(metric=METRIC_C2 if args.config == "c2" else METRIC, value=round(value, 4),
+                    unit="volumes/s" if args.config == "c2" else "volume-pairs/s", n_gpus=world, steps=args.steps,
                     warmup=args.warmup, ms_per_step=round(ms, 2), higher_is_better=True, scaling="weak",
                     vs_baseline=None, dtype="f32", data="synthetic (z-scored N(0,1) volumes, Bernoulli labels)",
-                    config=(dict(workload=f"C3: SwinFusion 3D lift, {args.size}^3 sMRI+fMRI pairs",
-                                 global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
-                                 patch=8, window=6, tokens_per_volume=args.size ** 3,
-                                 parallelism=f"dp{world}", checkpoint=args.checkpoint, graph=graph)
-                            if args.config == "c3" else
-                            dict(workload=f"C4: SwinCrossmodal3D composite, {args.size}^3 pairs, crossmodal head "
-                                          f"12 layers x 12 heads on {(args.size // 8) ** 3}-token sequences",
-                                 global_batch=args.batch * world, per_gpu_batch=args.batch, volume=args.size,
-                                 patch=8, window=6, sequence=(args.size // 8) ** 3, parallelism=f"dp{world}",
-                                 checkpoint=args.checkpoint, graph=graph)),
+                    config=config,
                     roofline=roofline, cpu_baseline=cpu, loss=round(loss_v, 5),
                     kernels={k: dict(launches=v["launches"], avg_ms=round(v["avg_ms"], 4),
                                      total_ms=round(v["total_ms"], 2)) for k, v in kern.items()},

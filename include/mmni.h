@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 2
+#define MMNI_ABI_VERSION 3
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -151,11 +151,15 @@ typedef struct mmni_conv3d_desc {
    w is (Cout, Cin, kd, kh, kw) contiguous; 8-byte aligned for the k3 s1 p1 case (< 0 otherwise). */
 int mmni_conv3d_fwd(const mmni_conv3d_desc* d, const float* x, const float* w,
                     const float* bias, float* y, void* stream);
-/* dx overwritten (may be NULL); dw (Cout*Cin*kd*kh*kw) and db (Cout) ACCUMULATED (caller zeroes).
- * y is the forward output, needed when slope != 1 to gate the LeakyReLU gradient. */
+/* dx overwritten (may be NULL); dw (Cout*Cin*kd*kh*kw) and db (Cout, nullable) OVERWRITTEN.
+ * y is the forward output, needed when slope != 1 to gate the LeakyReLU gradient.
+ * workspace: >= mmni_conv3d_bwd_workspace_bytes(d) bytes, contents ignored: one row of partial
+ * dW/db per persistent workgroup, reduced in a fixed order, so dw/db are bitwise deterministic
+ * (ABI v3; v2 accumulated them with float atomics). */
+size_t mmni_conv3d_bwd_workspace_bytes(const mmni_conv3d_desc* d);
 int mmni_conv3d_bwd(const mmni_conv3d_desc* d, const float* x, const float* w,
                     const float* y, const float* dy, float* dx, float* dw, float* db,
-                    void* stream);
+                    void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Token-wise ops of the Swin blocks: LayerNorm over C = 12/24/48/96

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -76,7 +76,8 @@ SIGNATURES = {
     "mmni_mha_bwd": (_c_int, [ctypes.POINTER(MhaDesc)] + [_vp] * 11),
     "mmni_mha_mean_probs": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp]),
     "mmni_conv3d_fwd": (_c_int, [ctypes.POINTER(Conv3dDesc), _vp, _vp, _vp, _vp, _vp]),
-    "mmni_conv3d_bwd": (_c_int, [ctypes.POINTER(Conv3dDesc)] + [_vp] * 8),
+    "mmni_conv3d_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Conv3dDesc)]),
+    "mmni_conv3d_bwd": (_c_int, [ctypes.POINTER(Conv3dDesc)] + [_vp] * 9),
     "mmni_layernorm_fwd": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp]),
     "mmni_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
     "mmni_layernorm_bwd": (_c_int, [_c_i64, _c_int] + [_vp] * 10),

@@ -14,8 +14,9 @@
 //       LeakyReLU are fused into the epilogue.
 // dx  : one lane per input voxel (gather form of the transposed conv, no atomics).
 // dw  : output tiles staged in LDS with their input halo; each lane owns (tap, cin) pairs
-//       and all Cout accumulators; workgroups are persistent over tiles and flush their
-//       partial dW/db once with atomics.
+//       and all Cout accumulators; workgroups are persistent over tiles (a fixed tile set
+//       per block) and write their partial dW/db to a workspace row; a fixed-order column
+//       sum (tokenops.hip) reduces the rows, so dW/db are bitwise deterministic.
 #include "mmni_common.h"
 
 namespace mmni {
@@ -31,6 +32,7 @@ struct ConvArgs {
     float* dx;
     float* dw;
     float* db;
+    float* part;      // dw partials: [gridDim.x][Cout*Cin*K3 + Cout]
     // dw tiling
     int TZ, TY, TX, HZ, HY, HX, ntz, nty, ntx, ntiles;
 };
@@ -472,16 +474,19 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
         }
         flush = gi == 0;
     }
+    // this block's partial row; every column is written by exactly one lane of every block
+    const int ncw = npairs * COUT;
+    float* row = a.part + (int64_t)blockIdx.x * (ncw + COUT);
 #pragma unroll
     for (int m = 0; m < MAXP; ++m) {
         const int p = pl + m * 256;
         if (p < npairs && flush) {
             const int ci = p % CIN, t = p / CIN;
 #pragma unroll
-            for (int co = 0; co < COUT; ++co) atomicAdd(&a.dw[((int64_t)co * CIN + ci) * K3 + t], acc[m][co]);
+            for (int co = 0; co < COUT; ++co) row[((int64_t)co * CIN + ci) * K3 + t] = acc[m][co];
         }
     }
-    if (a.db && pl < COUT && flush) atomicAdd(&a.db[pl], dbs);
+    if (pl < COUT && flush) row[ncw + pl] = dbs;
 }
 
 static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
@@ -499,6 +504,41 @@ static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
     a.pd = d->pd; a.ph = d->ph; a.pw = d->pw;
     a.Do = d->Do; a.Ho = d->Ho; a.Wo = d->Wo;
     a.slope = d->slope;
+    return 0;
+}
+
+// dW tiling plan: output tile (TZ, TY, TX) shrunk until the LDS image (dz tile + input halo)
+// fits 64 KiB; persistent grid of at most kNumCU * MMNI_CONV_DW_BPC blocks.
+static int dw_plan(ConvArgs& a, int& grid, size_t& lds) {
+    const int CIN = a.Cin, COUT = a.Cout;
+    int TZ = 4, TY = 4, TX = 16;
+    auto hz = [&](int T) { return (T - 1) * a.sd + a.kd; };
+    auto hy = [&](int T) { return (T - 1) * a.sh + a.kh; };
+    auto hx = [&](int T) { return (T - 1) * a.sw + a.kw; };
+    if (a.Do == 1) TZ = 1;
+    auto bytes = [&]() {
+        return (size_t)(TZ * TY * TX * COUT + hz(TZ) * hy(TY) * hx(TX) * CIN) * 4;
+    };
+    while (bytes() > 64 * 1024) {
+        if (TX > 4) TX /= 2;
+        else if (TY > 1) TY /= 2;
+        else if (TZ > 1) TZ /= 2;
+        else if (TX > 1) TX /= 2;
+        else break;
+    }
+    MMNI_ARG_CHECK(bytes() <= 64 * 1024, "conv3d_dw: kernel too large for the LDS tile");
+    a.TZ = TZ; a.TY = TY; a.TX = TX;
+    a.HZ = hz(TZ); a.HY = hy(TY); a.HX = hx(TX);
+    a.ntz = (a.Do + TZ - 1) / TZ; a.nty = (a.Ho + TY - 1) / TY; a.ntx = (a.Wo + TX - 1) / TX;
+    a.ntiles = a.B * a.ntz * a.nty * a.ntx;
+    const int npairs = a.kd * a.kh * a.kw * CIN;
+    MMNI_ARG_CHECK(npairs <= 1024, "conv3d_dw: k^3*Cin = %d exceeds 1024 pairs", npairs);
+    grid = a.ntiles < kNumCU * MMNI_CONV_DW_BPC ? a.ntiles : kNumCU * MMNI_CONV_DW_BPC;
+    // the group reduction of the MAXP 1 kernel reuses the LDS image: [G][npairs][COUT] + [G][COUT]
+    const int G = npairs <= 256 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;
+    const size_t red = (size_t)G * (npairs + 1) * COUT * 4;
+    lds = bytes() > red ? bytes() : red;
+    MMNI_ARG_CHECK(lds <= 64 * 1024, "conv3d_dw: group reduction exceeds the LDS tile");
     return 0;
 }
 
@@ -528,37 +568,18 @@ static int conv_bwd_launch(ConvArgs& a, hipStream_t s) {
         int rc = launch_status("conv3d_dx");
         if (rc) return rc;
     }
-    // dw tile: shrink until the LDS image (dz tile + input halo) fits 64 KiB
-    int TZ = 4, TY = 4, TX = 16;
-    auto hz = [&](int T) { return (T - 1) * a.sd + a.kd; };
-    auto hy = [&](int T) { return (T - 1) * a.sh + a.kh; };
-    auto hx = [&](int T) { return (T - 1) * a.sw + a.kw; };
-    if (a.Do == 1) TZ = 1;
-    auto bytes = [&]() {
-        return (size_t)(TZ * TY * TX * COUT + hz(TZ) * hy(TY) * hx(TX) * CIN) * 4;
-    };
-    while (bytes() > 64 * 1024) {
-        if (TX > 4) TX /= 2;
-        else if (TY > 1) TY /= 2;
-        else if (TZ > 1) TZ /= 2;
-        else if (TX > 1) TX /= 2;
-        else break;
-    }
-    MMNI_ARG_CHECK(bytes() <= 64 * 1024, "conv3d_dw: kernel too large for the LDS tile");
-    a.TZ = TZ; a.TY = TY; a.TX = TX;
-    a.HZ = hz(TZ); a.HY = hy(TY); a.HX = hx(TX);
-    a.ntz = (a.Do + TZ - 1) / TZ; a.nty = (a.Ho + TY - 1) / TY; a.ntx = (a.Wo + TX - 1) / TX;
-    a.ntiles = a.B * a.ntz * a.nty * a.ntx;
+    int grid;
+    size_t lds;
+    int rc = dw_plan(a, grid, lds);
+    if (rc) return rc;
+    MMNI_ARG_CHECK(a.part != nullptr, "conv3d_bwd: null workspace");
     const int npairs = a.kd * a.kh * a.kw * CIN;
-    int grid = a.ntiles < kNumCU * MMNI_CONV_DW_BPC ? a.ntiles : kNumCU * MMNI_CONV_DW_BPC;
-    // the group reduction of the MAXP 1 kernel reuses the LDS image: [G][npairs][COUT] + [G][COUT]
-    const int G = npairs <= 256 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;
-    const size_t red = (size_t)G * (npairs + 1) * COUT * 4;
-    const size_t lds = bytes() > red ? bytes() : red;
-    MMNI_ARG_CHECK(lds <= 64 * 1024, "conv3d_dw: group reduction exceeds the LDS tile");
 #define MMNI_DW(MP)                                                                            \
     conv3d_dw_kernel<CIN, COUT, MP><<<grid, 256, lds, s>>>(a);                                 \
-    return launch_status("conv3d_dw");
+    rc = launch_status("conv3d_dw");                                                           \
+    if (rc) return rc;                                                                         \
+    column_sum(a.part, grid, npairs * COUT + COUT, a.dw, npairs * COUT, a.db, s);              \
+    return launch_status("conv3d_dw_colsum");
     if (npairs <= 256) { MMNI_DW(1) }
     if (npairs <= 512) { MMNI_DW(2) }
     if (npairs <= 768) { MMNI_DW(3) }
@@ -600,11 +621,21 @@ extern "C" int mmni_conv3d_fwd(const mmni_conv3d_desc* d, const float* x, const 
     MMNI_CONV_DISPATCH(conv_fwd_launch)
 }
 
+extern "C" size_t mmni_conv3d_bwd_workspace_bytes(const mmni_conv3d_desc* d) {
+    ConvArgs a{};
+    if (conv_fill(d, a)) return 0;
+    int grid;
+    size_t lds;
+    if (dw_plan(a, grid, lds)) return 0;
+    return (size_t)grid * (a.kd * a.kh * a.kw * a.Cin * a.Cout + a.Cout) * sizeof(float);
+}
+
 extern "C" int mmni_conv3d_bwd(const mmni_conv3d_desc* d, const float* x, const float* w, const float* y,
-                               const float* dy, float* dx, float* dw, float* db, void* stream) {
+                               const float* dy, float* dx, float* dw, float* db, void* workspace, void* stream) {
     ConvArgs a{};
     int rc = conv_fill(d, a);
     if (rc) return rc;
+    a.part = static_cast<float*>(workspace);
     MMNI_ARG_CHECK(x && w && dy && dw, "conv3d_bwd: null pointer");
     MMNI_ARG_CHECK(d->slope == 1.f || y != nullptr, "conv3d_bwd: LeakyReLU gradient needs y");
     a.x = x; a.w = w; a.y = const_cast<float*>(y); a.dy = dy; a.dx = dx; a.dw = dw; a.db = db;

@@ -346,6 +346,8 @@ class _Conv3d(torch.autograd.Function):
         require_device(x, weight, bias, what="conv3d")
         x = x.contiguous()
         weight = weight.contiguous()
+        if weight.data_ptr() % 8:
+            weight = weight.clone()   # the k3 kernel reads 8-B aligned weight pairs (mmni.h)
         assert weight.dim() == 5 and x.dim() == 5 and x.shape[-1] == weight.shape[1]
         d = _conv_desc(tuple(x.shape), tuple(weight.shape), stride, pad, slope)
         y = torch.empty((d.B, d.Do, d.Ho, d.Wo, d.Cout), device=x.device, dtype=torch.float32)
@@ -366,11 +368,13 @@ class _Conv3d(torch.autograd.Function):
         dy = dy.contiguous()
         d = _conv_desc(tuple(x.shape), tuple(weight.shape), stride, pad, slope)
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dw = torch.zeros_like(weight)
-        db = torch.zeros(d.Cout, device=x.device, dtype=torch.float32) if has_bias else None
+        dw = torch.empty_like(weight)
+        db = torch.empty(d.Cout, device=x.device, dtype=torch.float32) if has_bias else None
+        L = _lib.load()
+        ws = torch.empty(L.mmni_conv3d_bwd_workspace_bytes(d) // 4, device=x.device, dtype=torch.float32)
         ev = KernelTimer.start()
-        check(_lib.load().mmni_conv3d_bwd(d, ptr(x), ptr(weight), ptr(y), ptr(dy), ptr(dx), ptr(dw), ptr(db),
-                                           stream_handle(x.device)), "mmni_conv3d_bwd")
+        check(L.mmni_conv3d_bwd(d, ptr(x), ptr(weight), ptr(y), ptr(dy), ptr(dx), ptr(dw), ptr(db), ptr(ws),
+                                stream_handle(x.device)), "mmni_conv3d_bwd")
         nout = dy.numel() // d.Cout
         KernelTimer.stop(f"conv3d_bwd_{d.Cin}x{d.Cout}_k{d.kd}{d.kh}{d.kw}", ev,
                          4.0 * nout * d.Cout * d.Cin * d.kd * d.kh * d.kw,

@@ -64,12 +64,14 @@ def relative_index_buffer(window):
     return idx
 
 
-def shift_mask_buffer(resolution, window, shift):
-    """(nW, N, N) {0, -100} mask of one sample for a shifted-window layer of `resolution`."""
+def shift_label_windows(resolution, window, shift, device=None):
+    """(nW, N) region label of every window token of one sample: the labelled image of
+    calculate_mask (swinfusion_module.py:317-329) partitioned into windows; axes with shift 0
+    carry a single region (3D lift rule)."""
     nd = len(resolution)
-    label = torch.zeros(resolution, dtype=torch.long)
+    label = torch.zeros(resolution, dtype=torch.long, device=device)
     for a, (L, w, s) in enumerate(zip(resolution, window, shift)):
-        lab = torch.zeros(L, dtype=torch.long)
+        lab = torch.zeros(L, dtype=torch.long, device=device)
         if s > 0:
             lab[L - w:L - s] = 1
             lab[L - s:] = 2
@@ -80,9 +82,88 @@ def shift_mask_buffer(resolution, window, shift):
     for L, w in zip(resolution, window):
         split += [L // w, w]
     perm = [2 * a for a in range(nd)] + [2 * a + 1 for a in range(nd)]
-    win = label.view(split).permute(perm).reshape(-1, math.prod(window))
+    return label.view(split).permute(perm).reshape(-1, math.prod(window))
+
+
+def shift_mask_buffer(resolution, window, shift):
+    """(nW, N, N) {0, -100} mask of one sample for a shifted-window layer of `resolution`."""
+    win = shift_label_windows(resolution, window, shift)
     diff = win.unsqueeze(1) - win.unsqueeze(2)
     return torch.zeros(diff.shape).masked_fill(diff != 0, -100.0)
+
+
+def _factorizations(n, k):
+    if k == 1:
+        yield (n,)
+        return
+    for a in range(1, n + 1):
+        if n % a == 0:
+            for rest in _factorizations(n // a, k - 1):
+                yield (a,) + rest
+
+
+_MASK_GEOMETRY = {}
+
+
+def geometry_for_mask(mask, window):
+    """(resolution, shift) of a shifted-window layer whose calculate_mask equals `mask` (nW, N, N),
+    or None.  Validated once per mask tensor version (cached).  The attention of a window depends
+    only on its own tokens and mask[w mod nW], so any geometry reproducing the mask gives the
+    reference's result."""
+    window = tuple(int(w) for w in window)
+    key = (mask.data_ptr(), mask._version, tuple(mask.shape), window, str(mask.device))
+    if key in _MASK_GEOMETRY:
+        return _MASK_GEOMETRY[key]
+    nW, N, _ = mask.shape
+    found = None
+    m = mask.detach()
+    if N == math.prod(window):
+        for counts in _factorizations(nW, len(window)):
+            if any(c > 1 and w == 1 for c, w in zip(counts, window)):
+                continue
+            res = tuple(c * w for c, w in zip(counts, window))
+            for s in range(1, max(window)):
+                shift = tuple(s if w > s else 0 for w in window)
+                lab = shift_label_windows(res, window, shift, device=m.device)
+                ok = True
+                for w0 in range(0, nW, 256):
+                    lb = lab[w0:w0 + 256]
+                    cand = (lb.unsqueeze(1) != lb.unsqueeze(2)).to(m.dtype) * -100.0
+                    if not torch.equal(cand, m[w0:w0 + 256]):
+                        ok = False
+                        break
+                if ok:
+                    found = (res, shift)
+                    break
+            if found:
+                break
+    _MASK_GEOMETRY[key] = found
+    return found
+
+
+def attend_masked_windows(fn, windows, mask, window):
+    """Run a fused window-attention `fn(rows..., geom) -> rows` on PRE-PARTITIONED shifted windows
+    (num_windows*B, N, C) with the reference's explicit shift mask (WindowAttention*.forward(x, mask),
+    swinfusion_module.py:114,213; swin_v2_module.py:138).  The windows are put back into their
+    shifted frame, rolled back by the shift the mask encodes, attended by the kernel (which
+    re-applies the roll and derives the same mask analytically) and re-partitioned."""
+    from .swinfusion_module import window_partition_fusion, window_reverse_fusion
+    geo = geometry_for_mask(mask, window)
+    if geo is None:
+        raise NotImplementedError("window attention: the mask is not a shifted-window calculate_mask of any "
+                                  "geometry; the fused kernel derives masks analytically and takes no arbitrary ones")
+    res, shift = geo
+    nd = len(res)
+    B_, N, C = windows[0].shape
+    B = B_ // mask.shape[0]
+    dims = tuple(range(1, nd + 1))
+    rows = []
+    for t in windows:
+        xs = window_reverse_fusion(t.reshape(B_, *window, t.shape[-1]), window, *res)
+        rows.append(torch.roll(xs, shifts=shift, dims=dims).reshape(-1, t.shape[-1]))
+    out = fn(*rows, geometry(B, res, window, shift)).view(B, *res, C)
+    out = torch.roll(out, shifts=tuple(-s for s in shift), dims=dims)
+    return window_partition_fusion(out, window).reshape(B_, N, C)
 
 
 def clamp_window(input_resolution, window_size, shift_size):

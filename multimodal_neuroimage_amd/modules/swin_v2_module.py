@@ -17,7 +17,7 @@ import torch.utils.checkpoint as checkpoint
 
 from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear, mlp
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
-                      clamp_window, geometry, patch_merge_gather)
+                      attend_masked_windows, clamp_window, geometry, patch_merge_gather)
 
 
 class Mlp(nn.Module):
@@ -110,10 +110,10 @@ class WindowAttention(nn.Module):
         return self.proj_drop(linear(o, self.proj))
 
     def forward(self, x, mask=None):
-        """Reference signature on pre-partitioned windows (num_windows*B, N, C), no shift mask."""
+        """Reference signature on pre-partitioned windows (num_windows*B, N, C); a shift mask
+        (calculate_mask, (nW, N, N)) is validated once and mapped back to its geometry."""
         if mask is not None:
-            raise NotImplementedError("pass shifted windows through SwinTransformerBlock (the fused kernel derives "
-                                      "the mask from the geometry); explicit masks are not taken")
+            return attend_masked_windows(self.forward_tokens, [x], mask, self.window_size)
         B_, N, C = x.shape
         geom = geometry(B_, self.window_size, self.window_size, 0)
         return self.forward_tokens(x.reshape(B_ * N, C), geom).view(B_, N, C)

@@ -20,7 +20,7 @@ import torch.utils.checkpoint as checkpoint
 from ..functional import (window_attention_self, window_attention_cross, conv3d_cl, layer_norm, linear, mlp, ln_linear,
                           ln_linear_ok, ln_mlp)
 from ._common import (DropPath, inactive, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
-                      clamp_window, geometry, patch_merge_gather)
+                      attend_masked_windows, clamp_window, geometry, patch_merge_gather)
 
 
 class Mlp_fusion(nn.Module):
@@ -107,11 +107,11 @@ class WindowAttention_fusion(nn.Module):
         return out if residual is None else residual + out
 
     def forward(self, x, mask=None):
-        """Reference signature: x (num_windows*B, N, C) already partitioned (no shift mask).
-        Each window is attended as its own unshifted volume."""
+        """Reference signature: x (num_windows*B, N, C) already partitioned.  Without a mask each
+        window is attended as its own unshifted volume; a shift mask (calculate_mask of the block,
+        (nW, N, N)) is validated once and mapped back to the geometry the kernel derives it from."""
         if mask is not None:
-            raise NotImplementedError("pass shifted windows through SwinTransformerBlock_fusion (the fused "
-                                      "kernel derives the mask from the geometry); explicit masks are not taken")
+            return attend_masked_windows(self.forward_tokens, [x], mask, self.window_size)
         B_, N, C = x.shape
         geom = geometry(B_, self.window_size, self.window_size, 0)
         return self.forward_tokens(x.reshape(B_ * N, C), geom).view(B_, N, C)
@@ -160,8 +160,7 @@ class Cross_WindowAttention(nn.Module):
 
     def forward(self, x, y, mask=None):
         if mask is not None:
-            raise NotImplementedError("pass shifted windows through Cross_SwinTransformerBlock (the fused kernel "
-                                      "derives the mask from the geometry); explicit masks are not taken")
+            return attend_masked_windows(self.forward_tokens, [x, y], mask, self.window_size)
         B_, N, C = x.shape
         geom = geometry(B_, self.window_size, self.window_size, 0)
         return self.forward_tokens(x.reshape(B_ * N, C), y.reshape(B_ * N, C), geom).view(B_, N, C)

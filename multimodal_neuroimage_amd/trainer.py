@@ -21,6 +21,7 @@ in the way the reference's own dataset registry does.
 """
 import csv
 import os
+import warnings
 from itertools import zip_longest
 
 import numpy as np
@@ -406,6 +407,15 @@ class Trainer:
             self.writer.write_losses(loss_dict, set="train")
             if self.kwargs.get("profiling") and batch_idx == 10:
                 break
+        self.check_nans(f"epoch {epoch}")
+
+    def check_nans(self, where):
+        """One device read per epoch of the NaN flag the steps OR into (the reference checks every
+        step with a host sync and warns, trainer.py:548-555); warn the same way, then reset."""
+        if int(self.nan_flag.item()):
+            warnings.warn('found nans in computation')
+            print(f'at {where}: a training loss was NaN')
+            self.nan_flag.zero_()
 
     def eval_epoch(self, set):
         loader = self.val_loader if set == "val" else self.test_loader

@@ -30,15 +30,12 @@ def shifted_window_rows(batch, spatial, window, shift):
     return win.astype(np.int64)
 
 
-def shift_mask(spatial, window, shift):
-    """Shifted-window attention mask of one sample, values {0, -100}.
-
-    Restates calculate_mask (modules/swinfusion_module.py:317-338; modules/swin_v2_module.py:244-262):
-    regions of the shifted frame are labelled by the slices (0,-ws), (-ws,-s), (-s,None) per
-    axis (the cartesian product of per-axis labels), windows are partitioned, and token pairs
-    with different labels get -100.  Axes with shift 0 contribute a single region (the 3D lift
-    rule of SURVEY Q19).
-    """
+def shift_labels(spatial, window, shift):
+    """Per-window region labels of one sample, (nW, N) int64: the labelled image of
+    calculate_mask (modules/swinfusion_module.py:317-338; modules/swin_v2_module.py:244-262)
+    partitioned into windows.  Regions of the shifted frame are the slices (0,-ws), (-ws,-s),
+    (-s,None) per axis (the cartesian product of per-axis labels); axes with shift 0 contribute
+    a single region (the 3D lift rule of SURVEY Q19)."""
     spatial = tuple(spatial)
     nd = len(spatial)
     labels = np.zeros(spatial, dtype=np.int64)
@@ -54,7 +51,14 @@ def shift_mask(spatial, window, shift):
     for L, ws in zip(spatial, window):
         split += [L // ws, ws]
     order = [2 * a for a in range(nd)] + [2 * a + 1 for a in range(nd)]
-    win = labels.reshape(split).transpose(order).reshape(-1, int(np.prod(window)))
+    return labels.reshape(split).transpose(order).reshape(-1, int(np.prod(window)))
+
+
+def shift_mask(spatial, window, shift):
+    """Shifted-window attention mask of one sample, values {0, -100}: token pairs of a window
+    with different region labels (shift_labels) get -100 (calculate_mask,
+    modules/swinfusion_module.py:330-338)."""
+    win = shift_labels(spatial, window, shift)
     diff = win[:, None, :] - win[:, :, None]
     return np.where(diff != 0, -100.0, 0.0).astype(np.float32)
 

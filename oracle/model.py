@@ -52,7 +52,8 @@ def fusion_block(p, pre, x, x_size, heads, ws, shift):
     sp, win, sh = _grid(x_size, ws, shift)
     h = _ln(p, pre + ".norm1", x).reshape(-1, C)
     q, k, v = _lin(p, pre + ".attn.qkv", h).split(C, dim=-1)
-    o = O.window_attention(q, k, v, p[pre + ".attn.relative_position_bias_table"], B, sp, win, sh, heads, 0)
+    o = O.window_attention(q, k, v, p[pre + ".attn.relative_position_bias_table"], B, sp, win, sh, heads, 0,
+                           chunk=ATTN_CHUNK)
     x = x + _lin(p, pre + ".attn.proj", o).view(B, L, C)
     return x + _mlp(p, pre + ".mlp", _ln(p, pre + ".norm2", x))
 
@@ -66,7 +67,8 @@ def cross_block(p, pre, x, y, x_size, heads, ws, shift):
     def attend(att, a, b):
         q = _lin(p, att + ".q", a)
         k, v = _lin(p, att + ".kv", b).split(C, dim=-1)
-        o = O.window_attention(q, k, v, p[att + ".relative_position_bias_table"], B, sp, win, sh, heads, 0)
+        o = O.window_attention(q, k, v, p[att + ".relative_position_bias_table"], B, sp, win, sh, heads, 0,
+                               chunk=ATTN_CHUNK)
         return _lin(p, att + ".proj", o).view(B, L, C)
 
     xa = attend(pre + ".attn_A", xn, yn)
@@ -101,10 +103,11 @@ def v2_block(p, pre, x, res, heads, ws, shift):
     a = pre + ".attn"
     bias = torch.cat((p[a + ".q_bias"], torch.zeros_like(p[a + ".v_bias"]), p[a + ".v_bias"]))
     q, k, v = F.linear(x.reshape(-1, C), p[a + ".qkv.weight"], bias).split(C, dim=-1)
-    coords = torch.from_numpy(relative_coords_table(win)).to(x.dtype)
+    coords = torch.from_numpy(relative_coords_table(win)).to(x.device, x.dtype)
     table = O.swin_v2_bias_table((p[a + ".cpb_mlp.0.weight"], p[a + ".cpb_mlp.0.bias"], p[a + ".cpb_mlp.2.weight"]),
                                  coords, heads)
-    o = O.window_attention(q, k, v, table, B, sp, win, sh, heads, 1, tau=O.swin_v2_tau(p[a + ".logit_scale"]))
+    o = O.window_attention(q, k, v, table, B, sp, win, sh, heads, 1, tau=O.swin_v2_tau(p[a + ".logit_scale"]),
+                           chunk=ATTN_CHUNK)
     o = _lin(p, a + ".proj", o).view(B, L, C)
     x = x + _ln(p, pre + ".norm1", o)
     return x + _ln(p, pre + ".norm2", _mlp(p, pre + ".mlp", x))
@@ -235,7 +238,7 @@ def _embed_tokens(x_in):
     position_embedding.py:30-79); x_in (T, B, E)."""
     T, B, E = x_in.shape
     pos = O.sinusoidal_positions(x_in.transpose(0, 1)[:, :, 0])          # (B, T)
-    table = O.sinusoidal_table(T + 1, E).to(x_in.dtype)
+    table = O.sinusoidal_table(T + 1, E).to(x_in.device, x_in.dtype)
     return math.sqrt(E) * x_in + table[pos].transpose(0, 1)
 
 
@@ -303,6 +306,12 @@ def swin_crossmodal_logits(p, A, Bv, cfg):
     return logits
 
 
-def params_of(module, dtype=torch.float64):
+def params_of(module, dtype=torch.float64, device=None):
     """Detached parameter dict (leaf tensors, requires_grad) keyed like the state_dict."""
-    return {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in module.named_parameters()}
+    return {k: v.detach().to(device=device, dtype=dtype).clone().requires_grad_(True)
+            for k, v in module.named_parameters()}
+
+
+# windows per checkpointed chunk of every window-attention call in the functions above (None:
+# unchunked).  Tests that run the float64 oracle at full volume sizes on the GPU set it.
+ATTN_CHUNK = None

@@ -11,12 +11,13 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .index_maps import shifted_window_rows, shift_mask, relative_position_index
+from .index_maps import shifted_window_rows, shift_labels, relative_position_index
 
 LN100 = math.log(1.0 / 0.01)
 
 
-def window_attention(q, k, v, table, batch, spatial, window, shift, heads, kind=0, scale=None, tau=None):
+def window_attention(q, k, v, table, batch, spatial, window, shift, heads, kind=0, scale=None, tau=None,
+                     chunk=None):
     """Shifted-window attention on token rows.
 
     q, k, v: (batch*prod(spatial), C) token rows.  table: (Tsz, heads) additive bias table
@@ -26,38 +27,58 @@ def window_attention(q, k, v, table, batch, spatial, window, shift, heads, kind=
     Restates WindowAttention_fusion.forward (swinfusion_module.py:114-145),
     Cross_WindowAttention.forward (:213-246) and WindowAttention.forward (swin_v2_module.py:138-178)
     between their projections, plus the roll/partition/reverse of the blocks.
+
+    Runs on whatever device q lives on.  chunk (windows per chunk, optional): the attention is
+    evaluated chunk by chunk under activation checkpointing, so autograd keeps only the inputs and
+    recomputes one chunk's N x N logits at a time in backward; windows are independent, so the
+    result and every gradient are those of the unchunked computation.  This is what lets the
+    float64 oracle run at the full 4 x 96^3 bench geometry (16,384 windows) on the GPU.
     """
     spatial, window, shift = tuple(spatial), tuple(window), tuple(shift)
+    dev = q.device
     C = q.shape[1]
     hd = C // heads
     N = int(np.prod(window))
-    rows = torch.from_numpy(shifted_window_rows(batch, spatial, window, shift))
+    rows = torch.from_numpy(shifted_window_rows(batch, spatial, window, shift)).to(dev)
     nwin = rows.shape[0]
+    if kind == 0 and scale is None:
+        scale = hd ** -0.5
+    ridx = torch.from_numpy(relative_position_index(window)).reshape(-1).to(dev)
+    labels = None
+    if any(s > 0 for s in shift):
+        labels = torch.from_numpy(shift_labels(spatial, window, shift)).to(dev)
+    nW = nwin // batch
 
     def gather(t):
         return t[rows.reshape(-1)].reshape(nwin, N, heads, hd).permute(0, 2, 1, 3)
 
+    def core(qw, kw, vw, table, tau, w0):
+        if kind == 0:
+            logits = (qw * scale) @ kw.transpose(-2, -1)
+        else:
+            logits = F.normalize(qw, dim=-1) @ F.normalize(kw, dim=-1).transpose(-2, -1)
+            logits = logits * tau.reshape(1, heads, 1, 1)
+        bias = table[ridx].reshape(N, N, heads).permute(2, 0, 1)
+        logits = logits + bias.unsqueeze(0)
+        if labels is not None:
+            lab = labels[torch.arange(w0, w0 + qw.shape[0], device=dev) % nW]      # mask by w mod nW
+            mask = (lab[:, None, :] != lab[:, :, None]).to(logits.dtype) * -100.0
+            logits = logits + mask.unsqueeze(1)
+        p = torch.softmax(logits, dim=-1)
+        return (p @ vw).transpose(1, 2).reshape(qw.shape[0] * N, C)
+
     qw, kw, vw = gather(q), gather(k), gather(v)
-    if kind == 0:
-        if scale is None:
-            scale = hd ** -0.5
-        logits = (qw * scale) @ kw.transpose(-2, -1)
+    if chunk is None or chunk >= nwin:
+        ow = core(qw, kw, vw, table, tau, 0)
     else:
-        logits = F.normalize(qw, dim=-1) @ F.normalize(kw, dim=-1).transpose(-2, -1)
-        logits = logits * tau.reshape(1, heads, 1, 1)
-    ridx = torch.from_numpy(relative_position_index(window)).reshape(-1)
-    bias = table[ridx].reshape(N, N, heads).permute(2, 0, 1)
-    logits = logits + bias.unsqueeze(0)
-    if any(s > 0 for s in shift):
-        mask = torch.from_numpy(shift_mask(spatial, window, shift)).to(logits.dtype)
-        nW = mask.shape[0]
-        logits = logits.view(batch, nW, heads, N, N) + mask.unsqueeze(1).unsqueeze(0)
-        logits = logits.view(nwin, heads, N, N)
-    p = torch.softmax(logits, dim=-1)
-    ow = (p @ vw).transpose(1, 2).reshape(nwin * N, C)
-    out = torch.empty_like(q)
-    out = out.index_copy(0, rows.reshape(-1), ow)
-    return out
+        from torch.utils.checkpoint import checkpoint
+        parts = []
+        for w0 in range(0, nwin, chunk):
+            sl = slice(w0, min(w0 + chunk, nwin))
+            parts.append(checkpoint(core, qw[sl], kw[sl], vw[sl], table, tau, w0, use_reentrant=False))
+        ow = torch.cat(parts, 0)
+    out = torch.zeros_like(q)
+    return out.index_copy(0, rows.reshape(-1), ow)
 
 
 def swin_v2_tau(logit_scale):
@@ -91,7 +112,7 @@ def mha_core(q, k, v, heads, diag=0, scale=None):
     vh = v.reshape(Tk, B * heads, hd).transpose(0, 1)
     w = torch.bmm(qh, kh.transpose(1, 2))
     if diag > 0:
-        mask = torch.triu(torch.full((Tq, Tk), float("-inf"), dtype=w.dtype), diag)
+        mask = torch.triu(torch.full((Tq, Tk), float("-inf"), dtype=w.dtype, device=w.device), diag)
         w = w + mask.unsqueeze(0)
     w = torch.softmax(w, dim=-1)
     out = torch.bmm(w, vh).transpose(0, 1).reshape(Tq, B, E)
@@ -115,7 +136,7 @@ def sinusoidal_positions(tokens):
     """Positions for a (B, T) tensor: 1..T where tokens != 0, else 0 (make_positions,
     position_embedding.py:8-27, left_pad=0)."""
     B, T = tokens.shape
-    pos = torch.arange(1, T + 1).unsqueeze(0).expand(B, T)
+    pos = torch.arange(1, T + 1, device=tokens.device).unsqueeze(0).expand(B, T)
     return torch.where(tokens != 0, pos, torch.zeros_like(pos))
 
 

@@ -1,0 +1,133 @@
+"""Parity at the benchmark geometries themselves.
+
+* C3 kernel geometry: 4 x 96^3 tokens, 6^3 windows (16,384 windows, N = 216), shift 3 — the shape
+  bench.py times — for SwinFusion self attention, cross attention and Swin-V2 cosine attention,
+  forward and backward including the bias-table and tau gradients, against the float64 oracle
+  (oracle/ops.py: window_attention) run on the GPU in checkpointed window chunks.
+* A full-depth 3D SwinFusion (Ex [6, 6], Fusion 3 x [2, 2], Re [6, 6]: 60 window-attention blocks,
+  the C3 topology) at 48^3, B = 2: logits, input gradients and every parameter gradient against
+  the float64 oracle model (oracle/model.py), itself pinned to the reference's 2D fixtures.
+* C2: the single-modality 3D Swin-V2 (patch 8, depths [2, 2, 6], heads [3, 6, 12], 96^3 volumes,
+  B = 4, stage resolutions 12 -> 6 -> 3) against the same oracle.
+
+Tolerances: 1e-4 max-rel for single kernels (as test_kernels_gpu.py), 1e-3 for model logits and
+input gradients (north-star bar), 2e-3 for parameter gradients (as test_composite_gpu.py)."""
+import pytest
+import torch
+
+import recipe
+from multimodal_neuroimage_amd import functional as MF
+from multimodal_neuroimage_amd import model as M
+from oracle import model as OM
+from oracle import ops as O
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.detach().double(), b.detach().double().to(a.device)
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("kind,heads,cross", [(0, 6, False), (0, 6, True), (1, 3, False)])
+def test_window_attention_c3_geometry_vs_fp64_oracle(device, kind, heads, cross):
+    B, S, C = 4, 96, 12
+    spatial, window, shift = (S, S, S), (6, 6, 6), (3, 3, 3)
+    geom = MF.WindowGeometry(B, spatial, window, shift)
+    rows = geom.tokens
+    g = torch.Generator(device=device).manual_seed(1000 + 10 * kind + int(cross))
+    q, k, v, gout = (torch.randn(rows, C, device=device, generator=g) for _ in range(4))
+    table = torch.randn(geom.table_rows, heads, device=device, generator=g) * (0.5 if kind == 0 else 4.0)
+    tau = (torch.rand(heads, device=device, generator=g) * 15 + 5) if kind == 1 else None
+    scale = (C // heads) ** -0.5
+    # float64 oracle on the device, 512 windows per checkpointed chunk
+    leaves = [t.double().requires_grad_(True) for t in (q, k, v, table)]
+    tau_l = tau.double().requires_grad_(True) if tau is not None else None
+    ref = O.window_attention(*leaves, B, spatial, window, shift, heads, kind, scale=scale, tau=tau_l, chunk=512)
+    (ref * gout.double()).sum().backward()
+    # HIP kernels (fp32)
+    tab_d = table.clone().requires_grad_(True)
+    tau_d = tau.clone().requires_grad_(True) if tau is not None else None
+    if cross:
+        qd = q.clone().requires_grad_(True)
+        kvd = torch.cat([k, v], 1).requires_grad_(True)
+        out = MF.window_attention_cross(qd, kvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
+    else:
+        qkvd = torch.cat([q, k, v], 1).requires_grad_(True)
+        out = MF.window_attention_self(qkvd, tab_d, geom, heads, kind=kind, scale=scale, tau=tau_d)
+    (out * gout).sum().backward()
+    torch.cuda.synchronize()
+    if cross:
+        dq, dk, dv = qd.grad, kvd.grad[:, :C], kvd.grad[:, C:]
+    else:
+        dq, dk, dv = qkvd.grad[:, :C], qkvd.grad[:, C:2 * C], qkvd.grad[:, 2 * C:]
+    errs = dict(out=rel_err(out, ref), dq=rel_err(dq, leaves[0].grad), dk=rel_err(dk, leaves[1].grad),
+                dv=rel_err(dv, leaves[2].grad), dtable=rel_err(tab_d.grad, leaves[3].grad))
+    if tau is not None:
+        errs["dtau"] = rel_err(tau_d.grad, tau_l.grad)
+    assert max(errs.values()) < 1e-4, errs
+
+
+def _no_drop_path(m):
+    # the Swin-V2 head's hard-coded drop_path 0.1 (model.py:1188) is RNG: off for parity
+    for mod in m.modules():
+        if hasattr(mod, "drop_prob"):
+            mod.drop_prob = 0.0
+
+
+def _model_parity(device, m, ref_fn, inputs, tgt, ptol=2e-3):
+    recipe.fill_params(m)
+    _no_drop_path(m)
+    p = OM.params_of(m, torch.float64, device)
+    ins64 = [t.to(device).double().requires_grad_(True) for t in inputs]
+    OM.ATTN_CHUNK = 256
+    try:
+        ref = ref_fn(p, *ins64)
+        torch.nn.functional.binary_cross_entropy_with_logits(ref, tgt.to(device).double()).backward()
+    finally:
+        OM.ATTN_CHUNK = None
+    m = m.to(device)
+    ins = [t.to(device).requires_grad_(True) for t in inputs]
+    out = m(*ins)["binary_classification"]
+    torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device)).backward()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-3, (out, ref)
+    for a, r in zip(ins, ins64):
+        assert rel_err(a.grad, r.grad) < 1e-3
+    worst = {}
+    for k, prm in m.named_parameters():
+        r = p[k].grad
+        if r is None or float(r.abs().max()) == 0.0:
+            assert prm.grad is None or float(prm.grad.abs().max()) == 0.0, k
+            continue
+        worst[k] = rel_err(prm.grad, r)
+    bad = {k: e for k, e in worst.items() if e >= ptol}
+    assert not bad, bad
+    return worst
+
+
+def test_swinfusion3d_full_depth_48_vs_fp64_oracle(device):
+    """The C3 topology (60 window-attention blocks, conv stacks, Swin-V2 head) at 48^3, B = 2."""
+    kw = dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
+              attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=48, patch_size=4,
+              window_size=6, no_init_weights=True, volume_size=48)
+    m = M.SwinFusion(**kw)
+    A = torch.from_numpy(recipe.randn(8100, (2, 48, 48, 48)))
+    Bv = torch.from_numpy(recipe.randn(8101, (2, 48, 48, 48)))
+    cfg = dict(window_size=6, Ex_depths=[6, 6], Fusion_depths=[2, 2, 2], Re_depths=[6, 6], heads=6,
+               resolution=(12, 12, 12), head_patch=4)
+    worst = _model_parity(device, m, lambda p, a, b: OM.swinfusion_logits(p, a, b, cfg), [A, Bv],
+                          torch.tensor([[1.0], [0.0]]))
+    assert len(worst) > 300   # every trained tensor was compared
+
+
+def test_swin_v2_c2_96_b4_vs_fp64_oracle(device):
+    """C2: single-modality 3D Swin-V2, 96^3 volumes, B = 4 (stage resolutions 12 -> 6 -> 3)."""
+    kw = dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
+              attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=96, patch_size=8,
+              window_size=6, no_init_weights=True, volume_size=96)
+    m = M.SwinTransformerV2(**kw)
+    x = torch.from_numpy(recipe.randn(8200, (4, 96, 96, 96)))
+    worst = _model_parity(device, m, lambda p, a: OM.swin_v2_logits(p, "", a, 8, 6), [x],
+                          torch.tensor([[1.0], [0.0], [1.0], [1.0]]))
+    assert any("layers.2.blocks.5" in k for k in worst)

@@ -299,3 +299,36 @@ def test_model_crossmodal(golden, device):
     check(xl.grad, g["crossmodal.dxl"], tol=1e-3, what="dxl")
     check(xu.grad, g["crossmodal.dxu"], tol=1e-3, what="dxu")
     _grad_stats_check(golden, "crossmodal.", m, 2e-3)
+
+
+@pytest.mark.parametrize("name", ["f12s3", "f84s3", "c12s3", "v12s3"])
+def test_window_attention_reference_signature_with_mask(golden, device, name):
+    """WindowAttention*.forward(x_windows, mask) with the reference's explicit calculate_mask on
+    pre-rolled, pre-partitioned windows (swinfusion_module.py:114,213; swin_v2_module.py:138), as the
+    reference's blocks call it: same outputs and gradients as the fixture."""
+    from multimodal_neuroimage_amd.modules._common import shift_mask_buffer
+    case = wattn_meta(golden)[name]
+    g = golden("wattn.npz")
+    m = wattn_module(case).to(device)
+    x, y, gout = wattn_inputs(golden, name, case)
+    B, H, W, C = x.shape
+    ws, s = case["ws"], case["shift"]
+    mask = shift_mask_buffer((H, W), (ws, ws), (s, s)).to(device)
+    x = x.to(device).requires_grad_(True)
+    y = y.to(device).requires_grad_(True) if y is not None else None
+
+    def part(t):
+        return SF.window_partition_fusion(torch.roll(t, (-s, -s), (1, 2)), ws).reshape(-1, ws * ws, C)
+
+    if y is not None:
+        ow = m(part(x), part(y), mask=mask)
+    else:
+        ow = m(part(x), mask=mask)
+    out = torch.roll(SF.window_reverse_fusion(ow.view(-1, ws, ws, C), ws, H, W), (s, s), (1, 2))
+    (out * gout.to(device)).sum().backward()
+    check(out, g[name + ".out"], what="out")
+    check(x.grad, g[name + ".dx"], what="dx")
+    if y is not None:
+        check(y.grad, g[name + ".dy"], what="dy")
+    for k, p in m.named_parameters():
+        check(p.grad, g[f"{name}.d.{k}"], tol=2e-4, what=k)

@@ -201,6 +201,29 @@ def test_conv3d_fwd_bwd_vs_oracle(device, B, sp, Cin, Cout, k, stride, pad, slop
         assert rel_err(a.grad, r.grad) < TOL
 
 
+@pytest.mark.parametrize("Cin,Cout,sp,k,pad", [(24, 12, (40, 40, 40), 3, 1), (1, 6, (33, 34, 35), 3, 1),
+                                               (12, 6, (24, 24, 24), 3, 1), (1, 12, (96, 96, 96), 8, 0)])
+def test_conv3d_weight_grad_is_deterministic(device, Cin, Cout, sp, k, pad):
+    """conv dW/db: per-workgroup partial rows reduced in a fixed order (no float atomics), so two
+    identical backward passes agree bitwise (the DDP test's per-tensor 1e-4 bar depends on it)."""
+    torch.manual_seed(Cin * 31 + Cout)
+    x = torch.randn(2, *sp, Cin, device=device)
+    w = (torch.randn(Cout, Cin, k, k, k, device=device) * 0.1).requires_grad_(True)
+    b = torch.randn(Cout, device=device).requires_grad_(True)
+    stride = 1 if k == 3 else k
+    g = None
+    grads = []
+    for _ in range(3):
+        w.grad = b.grad = None
+        out = MF.conv3d_cl(x, w, b, stride, pad, 0.2 if k == 3 else 1.0)
+        if g is None:
+            g = torch.randn_like(out)
+        (out * g).sum().backward()
+        grads.append((w.grad.clone(), b.grad.clone()))
+    for gw, gb in grads[1:]:
+        assert torch.equal(gw, grads[0][0]) and torch.equal(gb, grads[0][1])
+
+
 LN = [(1000, 12), (70001, 12), (513, 24), (4099, 48), (300, 96)]
 
 

@@ -1,6 +1,7 @@
 """Oracle integer maps vs fixtures generated from the reference itself (bit-exact)."""
 import numpy as np
 import pytest
+import torch
 
 from oracle.index_maps import shifted_window_rows, shift_mask, relative_position_index, relative_coords_table
 
@@ -64,3 +65,16 @@ def test_3d_mask_region_count():
     assert (m[0] == 0).all()          # interior window: single region
     last = m[-1]                        # corner window: 8 regions of 27 tokens each
     assert ((last == 0).sum(axis=1) == 27).all()
+
+
+@pytest.mark.parametrize("res,window,shift", [((12, 18), (6, 6), (3, 3)), ((84, 84), (6, 6), (3, 3)),
+                                              ((12, 12, 18), (6, 6, 6), (3, 3, 3)), ((1, 12, 12), (1, 6, 6), (0, 2, 2))])
+def test_mask_geometry_recovered_from_calculate_mask(res, window, shift):
+    """The reference-signature path (forward(x_windows, mask)) maps a calculate_mask back to a
+    geometry whose analytic mask is identical."""
+    from multimodal_neuroimage_amd.modules._common import geometry_for_mask, shift_mask_buffer
+    mask = shift_mask_buffer(res, window, shift)
+    got = geometry_for_mask(mask, window)
+    assert got is not None
+    assert torch.equal(shift_mask_buffer(got[0], window, got[1]), mask)
+    assert geometry_for_mask(torch.randn(mask.shape), window) is None

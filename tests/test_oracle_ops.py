@@ -91,3 +91,30 @@ def test_oracle_conv3d_matches_torch_conv2d_at_depth_one():
     x_cl = x.permute(0, 2, 3, 1).unsqueeze(1)
     got = O.conv3d_cl(x_cl, conv.weight.unsqueeze(2), conv.bias, (1, 1, 1), (0, 1, 1), 0.2)
     close(got.squeeze(1).permute(0, 3, 1, 2).detach().numpy(), ref.detach().numpy(), tol=1e-6)
+
+
+@pytest.mark.parametrize("kind,spatial,window,shift,chunk", [
+    (0, (12, 12, 18), (6, 6, 6), (3, 3, 3), 5),
+    (1, (6, 12, 12), (3, 6, 6), (1, 3, 3), 3),
+    (0, (1, 12, 18), (1, 6, 6), (0, 3, 3), 4),
+])
+def test_chunked_oracle_equals_unchunked(kind, spatial, window, shift, chunk):
+    """The checkpointed window-chunked oracle (used at full 96^3 size on the GPU) returns the same
+    output and gradients as the one-shot restatement pinned by the fixtures above."""
+    B, C, heads = 2, 12, 3
+    g = torch.Generator().manual_seed(11)
+    T = B * int(np.prod(spatial))
+    Tsz = int(np.prod([2 * w - 1 for w in window]))
+    base = [torch.randn(T, C, generator=g, dtype=torch.float64) for _ in range(3)]
+    base.append(torch.randn(Tsz, heads, generator=g, dtype=torch.float64))
+    tau0 = torch.rand(heads, generator=g, dtype=torch.float64) * 10 + 1
+    gout = torch.randn(T, C, generator=g, dtype=torch.float64)
+    res = []
+    for ch in (None, chunk):
+        leaves = [t.clone().requires_grad_(True) for t in base]
+        tau = tau0.clone().requires_grad_(True) if kind == 1 else None
+        out = O.window_attention(*leaves, B, spatial, window, shift, heads, kind, tau=tau, chunk=ch)
+        (out * gout).sum().backward()
+        res.append([out.detach()] + [t.grad for t in leaves] + ([tau.grad] if tau is not None else []))
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, rtol=1e-12, atol=1e-12)
