@@ -772,7 +772,12 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
 extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
     WGeom g;
     if (make_geom(d, g)) return 0;
-    return (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16;   // + the two absmax words
+    const size_t fixed = (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16;   // + the two absmax words
+    if (d->heads > 0 && wattn_bc_supported(g, d->C, d->heads, d->kind)) {
+        const size_t b = wattn_bc_workspace_bytes(g, d->heads);
+        return b > fixed ? b : fixed;
+    }
+    return fixed;
 }
 
 extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const float* k, const float* v,
@@ -792,6 +797,11 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                        row_aligned(dout, d->o_stride, d->C) && row_aligned(dq, d->q_stride, d->C) &&
                        row_aligned(dk, d->k_stride, d->C) && row_aligned(dv, d->v_stride, d->C),
                    "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
+    if (wattn_bc_supported(a.g, d->C, d->heads, d->kind)) {
+        a.q = q; a.k = k; a.v = v; a.table = table; a.tau = table; a.lse = const_cast<float*>(lse);
+        a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtable;
+        return wattn_bc_backward(a, d->heads, dtable, workspace, (hipStream_t)stream);
+    }
     void *kf, *kb;
     int maxt;
     bool packed = false;

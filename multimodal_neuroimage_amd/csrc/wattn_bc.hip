@@ -1,0 +1,474 @@
+// Window-attention backward for head_dim 2, "row-broadcast" formulation (SURVEY §8 rows a1, a3;
+// reference: WindowAttention_fusion.forward swinfusion_module.py:114-145 and
+// Cross_WindowAttention.forward :213-246, whose autograd backward this replaces).
+//
+// Two kernels per call, one workgroup = one (window, head pair) at a time, persistent:
+//   pass A  (wattn_bwdA_bc_kernel)  lane = query pair (t, t + N/2)  ->  dq and the bias-table gradient
+//   pass B  (wattn_bwdB_bc_kernel)  lane = key pair   (t, t + N/2)  ->  dk and dv
+// Every lane of a wave walks the SAME other-side row pair at each step (keys in pass A, queries in
+// pass B): those rows are LDS broadcast reads, and the per-lane work per (query, key, head pair)
+// is the bare recompute + gradient on packed fp32: no online reductions, no cross-lane traffic.
+//
+// LDS facts that shape it (measured here, gfx950): a same-address ds_read_b128 does NOT broadcast
+// (it ran ~16x slower than an 8-byte broadcast), so broadcast rows are stored as separate 8-byte
+// component arrays more than 2040 B apart (out of ds_read2_b64's offset reach), and every
+// component is one ds_read_b64.  The window is a compile-time shape (6^3 at the C3 geometry), so
+// the key/query coordinates and codes are scalar loop counters, and every table access of a step
+// is one address register plus immediate offsets.
+//
+// Bias-table gradient without atomics.  At one step the wave's lanes hold distinct queries against
+// the same key pair, so the relative-position entries they update, code(q) - code(k) + off, are
+// pairwise distinct (with the paired rows: entries E0, E0 - d, E0 + d, d = code(N/2), and no two
+// lanes' sets intersect because no two of their queries are N/2 apart).  Each wave therefore
+// read-modify-writes its OWN fp32 copy of the table in LDS with plain loads and stores: no atomics,
+// no fixed-point scale, no max|dO| pre-pass.  A workgroup always serves the same head pair; its
+// waves' copies are summed in a fixed order at the end into one partial row per workgroup, and a
+// fixed-order column sum (tokenops.hip) adds the rows: bitwise deterministic.
+//
+// Kind 0 only (scaled dot + table bias), one head pair (4 channels) per workgroup, windows with an
+// even first extent (N/2 = whole planes).
+#include "wattn_common.h"
+
+namespace mmni {
+
+namespace bc {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 splat(float x) { return (f2){x, x}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 exp2_2(f2 x) { return (f2){fast_exp2(x.x), fast_exp2(x.y)}; }
+
+// one head pair of a row in "pk" order: x[c] = (head 0 dim c, head 1 dim c); global rows hold
+// (h0 c0, h0 c1, h1 c0, h1 c1)
+struct Row {
+    f2 x[2];
+};
+
+__device__ __forceinline__ Row load_row_pk(const float* src) {
+    const float4 t = *reinterpret_cast<const float4*>(src);
+    Row r;
+    r.x[0] = (f2){t.x, t.z};
+    r.x[1] = (f2){t.y, t.w};
+    return r;
+}
+
+__device__ __forceinline__ void store_row_nat(float* dst, const Row& r, float scale) {
+    *reinterpret_cast<float4*>(dst) =
+        make_float4(r.x[0].x * scale, r.x[1].x * scale, r.x[0].y * scale, r.x[1].y * scale);
+}
+
+// (window, head pair) items: the NHG head-pair workgroups of a window sit 8 block indices apart,
+// i.e. on one XCD (blocks are dealt round-robin over the 8 XCDs), so a window's rows are fetched
+// from HBM once into that XCD's L2.  The grid is a multiple of 8 * NHG.
+struct Items {
+    int hp, first, stride;
+};
+
+__device__ __forceinline__ Items items(int NHG) {
+    Items it;
+    const int xslot = blockIdx.x >> 3;
+    it.hp = xslot % NHG;
+    it.first = (xslot / NHG) * 8 + (blockIdx.x & 7);
+    it.stride = gridDim.x / NHG;
+    return it;
+}
+
+constexpr int kThreads = 128;   // two waves: N / 2 <= 128 row pairs
+// f2 stride between the broadcast component arrays: > 255 f2 (2040 B, the reach of ds_read2_b64's
+// offsets), so the compiler keeps every component its own ds_read_b64
+constexpr int kSA = 264;
+
+// compile-time window (WD even): tokens t = (i*WH + j)*WW + k, relative codes
+// code = i*TW + j*TH + k, table rows TSZ, the second half starts DC codes later
+template <int WD, int WH, int WW>
+struct Win {
+    static constexpr int N = WD * WH * WW, H = N / 2;
+    static constexpr int TH = 2 * WW - 1, TW = (2 * WH - 1) * TH, TSZ = (2 * WD - 1) * TW;
+    static constexpr int OFF = (WD - 1) * TW + (WH - 1) * TH + (WW - 1);
+    static constexpr int DC = (WD / 2) * TW;
+    static_assert(WD % 2 == 0, "pairing needs whole planes");
+};
+
+// Per-window shift-region state.  A window spans several regions only if it is the last one
+// along a shifted axis (shift_region); then the region of local coordinate c on that axis is
+// 1 + (c >= w - s).  The region code packs one split bit per axis.
+struct Regions {
+    bool masked;
+    int lz, ly, lx;   // split points (local coordinate), or a value beyond the window (no split)
+};
+
+__device__ __forceinline__ Regions window_regions(const WGeom& g, int w) {
+    const int wx = w % g.nWw;
+    w /= g.nWw;
+    const int wy = w % g.nWh;
+    w /= g.nWh;
+    const int wz = w % g.nWd;
+    Regions r;
+    const bool mz = g.sd && wz == g.nWd - 1, my = g.sh && wy == g.nWh - 1, mx = g.sw && wx == g.nWw - 1;
+    r.masked = mz || my || mx;
+    r.lz = mz ? g.wd - g.sd : 1 << 20;
+    r.ly = my ? g.wh - g.sh : 1 << 20;
+    r.lx = mx ? g.ww - g.sw : 1 << 20;
+    return r;
+}
+
+__device__ __forceinline__ int region_code(const Regions& r, int i, int j, int k) {
+    return ((i >= r.lz) << 2) | ((j >= r.ly) << 1) | (k >= r.lx);
+}
+
+}  // namespace bc
+
+using bc::f2;
+using bc::Row;
+
+// ------------------------------------------------------------------------------------
+// pass A: lane = query pair (t, t + H); keys (n, n + H) broadcast; dq + private table gradient
+// ------------------------------------------------------------------------------------
+// LDS tables, TSZ entries of one f2 (the head pair) each: bias * log2 e, then wave 0's and wave
+// 1's table gradients, TSZ * 8 B apart (beyond ds_read2_b64's reach: each access stays one
+// ds_read_b64 / ds_write_b64), all addressed from one lane register plus immediates.
+template <int WD, int WH, int WW, int WAVE, bool MASKED>
+__device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2], const f2 (&lse2)[2],
+                                          const f2 (&ndl)[2], Row (&dq)[2], int cq, const int (&rq)[2],
+                                          const bc::Regions& reg, float* tabdt, const float* kv_s) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int EB = 8;                           // entry bytes
+    constexpr int DTO = (1 + WAVE) * Wn::TSZ * EB;  // this wave's table gradient
+    char* tb = reinterpret_cast<char*>(tabdt);
+    // lane address of entry (cq - code(n) - DC) = E- for code(n) = 0; E0 / E+ at +DC / +2 DC entries
+    const uint32_t lane_base = (uint32_t)((cq - Wn::DC) * EB);
+    const f2* kv2 = reinterpret_cast<const f2*>(kv_s);
+    int n = 0;
+    for (int i = 0; i < WD / 2; ++i) {
+        for (int j = 0; j < WH; ++j) {
+#pragma unroll
+            for (int k = 0; k < WW; ++k, ++n) {
+                const int code = i * Wn::TW + j * Wn::TH + k;
+                char* pm = tb + (lane_base - (uint32_t)(code * EB));   // entry E-  (query t, key n + H)
+                f2 kk[2][2], vv[2][2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        kk[v][c] = kv2[(v * 4 + c) * bc::kSA + n];
+                        vv[v][c] = kv2[(v * 4 + 2 + c) * bc::kSA + n];
+                    }
+                const f2 tbm = *reinterpret_cast<const f2*>(pm);
+                const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
+                const f2 tbp = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
+                int rk[2] = {0, 0};
+                if (MASKED) {
+                    rk[0] = bc::region_code(reg, i, j, k);
+                    rk[1] = bc::region_code(reg, i + WD / 2, j, k);
+                }
+                f2 ds[2][2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
+                        f2 base = t - lse2[u];
+                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                        f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                        s = bc::pfma(q[u].x[1], kk[v][1], s);
+                        const f2 p = bc::exp2_2(s);
+                        f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
+                        tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
+                        ds[u][v] = p * tt;
+                        dq[u].x[0] = bc::pfma(ds[u][v], kk[v][0], dq[u].x[0]);
+                        dq[u].x[1] = bc::pfma(ds[u][v], kk[v][1], dq[u].x[1]);
+                    }
+                }
+                // private table: plain read-modify-write (no two lanes of the wave share an entry
+                // at one step).  Lanes DO share entries across consecutive steps (lane t at key n + 1
+                // reads what lane t - 1 wrote at key n), a cross-lane order the compiler cannot see:
+                // the accesses are volatile so no read moves above an earlier step's write.
+                volatile f2* dm = reinterpret_cast<volatile f2*>(pm + DTO);
+                volatile f2* d0 = reinterpret_cast<volatile f2*>(pm + Wn::DC * EB + DTO);
+                volatile f2* dp = reinterpret_cast<volatile f2*>(pm + 2 * Wn::DC * EB + DTO);
+                const f2 om = *dm, o0 = *d0, op = *dp;
+                *d0 = o0 + (ds[0][0] + ds[1][1]);
+                *dm = om + ds[0][1];
+                *dp = op + ds[1][0];
+            }
+        }
+    }
+}
+
+template <int WD, int WH, int WW>
+__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int H = Wn::H, TSZ = Wn::TSZ;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    float* tabdt = smem;                          // [3][TSZ] f2: bias pair, dt wave 0, dt wave 1
+    float* kv_s = tabdt + TSZ * 6;                // [8][kSA] f2: k c0, k c1, v c0, v c1 of keys n, then n + H
+    const bc::Items it = bc::items(NHG);
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const bool lane_ok = tid < H;
+    const int t = lane_ok ? tid : 0;
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
+        tabdt[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
+        tabdt[TSZ * 2 + e] = 0.f;
+        tabdt[TSZ * 4 + e] = 0.f;
+    }
+    const int coff = it.hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    for (int w = it.first; w < g.nwin; w += it.stride) {
+        __syncthreads();   // previous window's K/V reads done (and the table staged, first time)
+        Row q[2], dO[2], dq[2];
+        f2 lse2[2], ndl[2];
+        int cq = 0, rq[2] = {0, 0};
+        int64_t row[2] = {0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int tt = t + u * H;
+                const TokenInfo ti = token_info(g, w, tt);
+                row[u] = ti.row;
+                rq[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
+                if (u == 0) cq = ti.code + Wn::OFF;
+                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
+                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
+                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * it.hp], a.lse[ti.row * NHT + 2 * it.hp + 1]} * kLog2e;
+                f2* kv2 = reinterpret_cast<f2*>(kv_s) + u * 4 * bc::kSA + t;
+                kv2[0] = (f2){kr.x, kr.z};
+                kv2[bc::kSA] = (f2){kr.y, kr.w};
+                kv2[2 * bc::kSA] = (f2){vr.x, vr.z};
+                kv2[3 * bc::kSA] = (f2){vr.y, vr.w};
+                dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
+            }
+        }
+        __syncthreads();
+        if (lane_ok) {
+            if (reg.masked) {
+                if (wave == 0) bwdA_loop<WD, WH, WW, 0, true>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
+                else bwdA_loop<WD, WH, WW, 1, true>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
+            } else {
+                if (wave == 0) bwdA_loop<WD, WH, WW, 0, false>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
+                else bwdA_loop<WD, WH, WW, 1, false>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) bc::store_row_nat(a.dq + row[u] * a.qs + coff, dq[u], a.scale);
+        }
+    }
+    __syncthreads();
+    // this workgroup's partial row: its head pair's columns (wave 0 + wave 1, fixed order), zeros in
+    // the other head pairs' columns
+    float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
+    for (int e = tid; e < TSZ * NHT; e += blockDim.x) {
+        const int r = e / NHT, c = e - r * NHT;
+        float v = 0.f;
+        if ((c >> 1) == it.hp) v = tabdt[TSZ * 2 + r * 2 + (c & 1)] + tabdt[TSZ * 4 + r * 2 + (c & 1)];
+        prow[e] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// pass B: lane = key pair (t, t + H); queries (n, n + H) broadcast; dk, dv
+// ------------------------------------------------------------------------------------
+template <int WD, int WH, int WW, bool MASKED>
+__device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2], Row (&dk)[2], Row (&dv)[2],
+                                          int ck, const int (&rk)[2], const bc::Regions& reg, const float* tab_s,
+                                          const float* rs_s) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int EB = 8;
+    const char* tb = reinterpret_cast<const char*>(tab_s);
+    // entry of (query n, key t) = code(n) + ck, ck = OFF - code(t); (n, t + H) is DC lower,
+    // (n + H, t) DC higher
+    const uint32_t lane_base = (uint32_t)((ck - Wn::DC) * EB);
+    const f2* rs2 = reinterpret_cast<const f2*>(rs_s);
+    int n = 0;
+    for (int i = 0; i < WD / 2; ++i) {
+        for (int j = 0; j < WH; ++j) {
+#pragma unroll
+            for (int k = 0; k < WW; ++k, ++n) {
+                const int code = i * Wn::TW + j * Wn::TH + k;
+                const char* pm = tb + (lane_base + (uint32_t)(code * EB));   // (n, t + H)
+                f2 qq[2][2], gg[2][2], ls[2], nd[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const f2* src = rs2 + u * 6 * bc::kSA + n;
+                    qq[u][0] = src[0];
+                    qq[u][1] = src[bc::kSA];
+                    gg[u][0] = src[2 * bc::kSA];
+                    gg[u][1] = src[3 * bc::kSA];
+                    ls[u] = src[4 * bc::kSA];
+                    nd[u] = src[5 * bc::kSA];
+                }
+                const f2 tbm = *reinterpret_cast<const f2*>(pm);
+                const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
+                const f2 tbp = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
+                int rq[2] = {0, 0};
+                if (MASKED) {
+                    rq[0] = bc::region_code(reg, i, j, k);
+                    rq[1] = bc::region_code(reg, i + WD / 2, j, k);
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {       // query n + u H
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {   // key t + v H
+                        const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
+                        f2 base = t - ls[u];
+                        if (MASKED) base += bc::splat(rq[u] == rk[v] ? 0.f : kMask2);
+                        f2 s = bc::pfma(qq[u][0], kr[v].x[0], base);
+                        s = bc::pfma(qq[u][1], kr[v].x[1], s);
+                        const f2 p = bc::exp2_2(s);
+                        f2 tt = bc::pfma(gg[u][0], vr[v].x[0], nd[u]);
+                        tt = bc::pfma(gg[u][1], vr[v].x[1], tt);
+                        const f2 dsv = p * tt;
+                        dv[v].x[0] = bc::pfma(p, gg[u][0], dv[v].x[0]);
+                        dv[v].x[1] = bc::pfma(p, gg[u][1], dv[v].x[1]);
+                        dk[v].x[0] = bc::pfma(dsv, qq[u][0], dk[v].x[0]);
+                        dk[v].x[1] = bc::pfma(dsv, qq[u][1], dk[v].x[1]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int WD, int WH, int WW>
+__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(3)))
+void wattn_bwdB_bc_kernel(WAArgs a) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int H = Wn::H, TSZ = Wn::TSZ;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    float* tab_s = smem;                            // [TSZ][2] bias * log2e of the head pair
+    float* rs_s = tab_s + TSZ * 2;                  // [12][kSA] f2: q2 c0, q2 c1, dO c0, dO c1, lse2, -delta
+    const bc::Items it = bc::items(NHG);
+    const int tid = threadIdx.x;
+    const bool lane_ok = tid < H;
+    const int t = lane_ok ? tid : 0;
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab_s[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
+    const int coff = it.hp * 4;
+    const float qs2 = a.scale * kLog2e;
+    for (int w = it.first; w < g.nwin; w += it.stride) {
+        __syncthreads();
+        Row kr[2], vr[2], dk[2], dv[2];
+        int ck = 0, rk[2] = {0, 0};
+        int64_t row[2] = {0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int tt = t + u * H;
+                const TokenInfo ti = token_info(g, w, tt);
+                row[u] = ti.row;
+                rk[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
+                if (u == 0) ck = Wn::OFF - ti.code;
+                kr[u] = bc::load_row_pk(a.k + ti.row * a.ks + coff);
+                vr[u] = bc::load_row_pk(a.v + ti.row * a.vs + coff);
+                dk[u].x[0] = dk[u].x[1] = dv[u].x[0] = dv[u].x[1] = bc::splat(0.f);
+                const float4 qr = *reinterpret_cast<const float4*>(a.q + ti.row * a.qs + coff);
+                const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti.row * a.os + coff);
+                const float4 orow = *reinterpret_cast<const float4*>(a.o + ti.row * a.os + coff);
+                const float l0 = a.lse[ti.row * NHT + 2 * it.hp], l1 = a.lse[ti.row * NHT + 2 * it.hp + 1];
+                f2* dst = reinterpret_cast<f2*>(rs_s) + u * 6 * bc::kSA + t;
+                const float d0 = orow.x * gr.x + orow.y * gr.y, d1 = orow.z * gr.z + orow.w * gr.w;
+                dst[0] = (f2){qr.x * qs2, qr.z * qs2};
+                dst[bc::kSA] = (f2){qr.y * qs2, qr.w * qs2};
+                dst[2 * bc::kSA] = (f2){gr.x, gr.z};
+                dst[3 * bc::kSA] = (f2){gr.y, gr.w};
+                dst[4 * bc::kSA] = (f2){l0 * kLog2e, l1 * kLog2e};
+                dst[5 * bc::kSA] = (f2){-d0, -d1};
+            }
+        }
+        __syncthreads();
+        if (lane_ok) {
+            if (reg.masked) bwdB_loop<WD, WH, WW, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+            else bwdB_loop<WD, WH, WW, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                bc::store_row_nat(a.dv + row[u] * a.vs + coff, dv[u], 1.0f);
+                bc::store_row_nat(a.dk + row[u] * a.ks + coff, dk[u], kLn2);   // staged q2 = q * scale * log2e
+            }
+        }
+    }
+}
+
+__global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) dtable[e] += src[e];
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+// The broadcast backward covers kind 0, head_dim 2, an even head count and the compiled window
+// shapes (6^3: the C3 geometry).
+bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind) {
+    if (kind != 0 || C != 2 * heads || heads % 2 != 0) return false;
+    return g.wd == 6 && g.wh == 6 && g.ww == 6;
+}
+
+static size_t bcA_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 6 * 4 + (size_t)8 * bc::kSA * 8; }
+static size_t bcB_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)12 * bc::kSA * 8; }
+
+static int bc_blocks(size_t lds, int NHG) {
+    int per_cu = (int)((160 * 1024) / lds);
+    if (per_cu > 16) per_cu = 16;
+    if (per_cu < 1) per_cu = 1;
+    int grid = kNumCU * per_cu;
+    grid -= grid % (8 * NHG);
+    return grid < 8 * NHG ? 8 * NHG : grid;
+}
+
+size_t wattn_bc_workspace_bytes(const WGeom& g, int heads) {
+    const int gridA = bc_blocks(bcA_lds(), heads / 2);
+    return ((size_t)gridA + 1) * g.Tsz * heads * sizeof(float);
+}
+
+static int set_lds_limit(const void* fn, size_t bytes) {
+    if (bytes <= 64 * 1024) return 0;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) {
+        set_error("hipFuncSetAttribute: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipStream_t s) {
+    const WGeom& g = a.g;
+    constexpr int kTsz666 = bc::Win<6, 6, 6>::TSZ;
+    MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_bwd (broadcast): compiled for 6^3 windows");
+    const int NHG = heads / 2;
+    a.hsplit = NHG;
+    const size_t ldsA = bcA_lds(), ldsB = bcB_lds();
+    const int gridA = bc_blocks(ldsA, NHG), gridB = bc_blocks(ldsB, NHG);
+    const void* kA = reinterpret_cast<const void*>(&wattn_bwdA_bc_kernel<6, 6, 6>);
+    const void* kB = reinterpret_cast<const void*>(&wattn_bwdB_bc_kernel<6, 6, 6>);
+    int rc = set_lds_limit(kA, ldsA);
+    if (rc) return rc;
+    rc = set_lds_limit(kB, ldsB);
+    if (rc) return rc;
+    const int ncol = g.Tsz * heads;
+    float* part = static_cast<float*>(workspace);          // [gridA][Tsz * heads]
+    float* sum = part + (size_t)gridA * ncol;              // [Tsz * heads]
+    wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
+    rc = launch_status("wattn_bwdA_bc");
+    if (rc) return rc;
+    wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
+    rc = launch_status("wattn_bwdB_bc");
+    if (rc) return rc;
+    column_sum(part, gridA, ncol, sum, ncol, nullptr, s);
+    rc = launch_status("wattn_bwd_dtable_sum");
+    if (rc) return rc;
+    wattn_dtable_add_kernel<<<(ncol + 255) / 256, 256, 0, s>>>(sum, dtable, ncol);
+    return launch_status("wattn_bwd_dtable_add");
+}
+
+}  // namespace mmni

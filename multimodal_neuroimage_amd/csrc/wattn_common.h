@@ -135,6 +135,11 @@ constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (pa
 int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
                      int& qpl_b, int& hs_b, int& hs_f);
 
+// Row-broadcast head_dim-2 backward (wattn_bc.hip): kind 0, head pairs, paired rows t, t + N/2.
+bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind);
+size_t wattn_bc_workspace_bytes(const WGeom& g, int heads);
+int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipStream_t s);
+
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
 // backward on gfx950 (measured: 27.8 ms vs 4.8 ms without the table update at the C3 shape),
