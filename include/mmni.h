@@ -109,29 +109,40 @@ int mmni_relative_index(const mmni_wattn_desc* d, int32_t* idx, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Crossmodal multi-head attention core:
- *   modules/multihead_attention.py:51-134 between in_proj and out_proj:
- *   softmax_fp32(q*scale @ k^T + mask) @ v, mask = -inf where (j - i) >= causal_diag
+ *   modules/multihead_attention.py:109-125 between in_proj and out_proj:
+ *   dropout(softmax_fp32(q*scale @ k^T + mask)) @ v, mask = -inf where (j - i) >= causal_diag
  *   (buffered_future_mask, crossmodal_transformer.py:179-186, causal_diag = 1+|Tk-Tq|).
  * Time-major layout (T, B, E): element (t, b, h, c) at ptr[(t*B + b)*stride + h*head_dim + c].
+ * head_dim 1..16 (padded to 4 / 8 / 16 on the f32 MFMA).
+ * Attention dropout (multihead_attention.py:123, F.dropout of the probabilities): dropout = p in
+ * [0, 1); element (b, h, i, j) is kept iff a counter-based hash of (seed, (b*heads + h)*Tq + i, j)
+ * falls below (1 - p) * 2^32, and kept probabilities are scaled by 1 / (1 - p).  The same seed in
+ * the backward regenerates the same mask.  p = 0 is the exact no-dropout path.  (ABI v3 added
+ * dropout and seed.)
  * ------------------------------------------------------------------------------------ */
 typedef struct mmni_mha_desc {
     int32_t Tq, Tk, B, heads, head_dim;
     int32_t causal_diag;        /* <= 0: no mask                                          */
     float   scale;              /* head_dim^-0.5 (multihead_attention.py:22)              */
     int64_t q_stride, k_stride, v_stride, o_stride;
+    float   dropout;            /* attention-probability dropout p (0: none)              */
+    uint32_t seed;              /* dropout stream; forward and backward must agree         */
 } mmni_mha_desc;
 
-/* out: (Tq, B, E) rows with o_stride; lse: (B, heads, Tq). */
+/* out: (Tq, B, E) rows with o_stride; lse: (B, heads, Tq) of the undropped softmax. */
 int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
                  float* out, float* lse, void* stream);
 /* dq/dk/dv overwritten; workspace: (B, heads, Tq) floats for delta = rowsum(dO*O). */
 int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
                  const float* out, const float* dout, const float* lse,
                  float* dq, float* dk, float* dv, float* workspace, void* stream);
-/* Head-averaged attention probabilities (B, Tq, Tk) — the second return value of
+/* Head-averaged (dropped) attention probabilities (B, Tq, Tk) — the second return value of
  * MultiheadAttention.forward (multihead_attention.py:131-133). */
 int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const float* k,
                         const float* lse, float* probs, void* stream);
+/* The dropout multipliers (0 or 1/(1-p)) of every (b, h, i, j) as (B, heads, Tq, Tk) floats:
+ * the mask the forward and backward apply, exported for tests. */
+int mmni_mha_dropout_mask(const mmni_mha_desc* d, float* mask, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * 3D convolutions.  Channels-last activations (B, D, H, W, C).

@@ -35,7 +35,8 @@ class WAttnDesc(ctypes.Structure):
 class MhaDesc(ctypes.Structure):
     _fields_ = [("Tq", _c_i32), ("Tk", _c_i32), ("B", _c_i32), ("heads", _c_i32), ("head_dim", _c_i32),
                 ("causal_diag", _c_i32), ("scale", _c_f),
-                ("q_stride", _c_i64), ("k_stride", _c_i64), ("v_stride", _c_i64), ("o_stride", _c_i64)]
+                ("q_stride", _c_i64), ("k_stride", _c_i64), ("v_stride", _c_i64), ("o_stride", _c_i64),
+                ("dropout", _c_f), ("seed", ctypes.c_uint32)]
 
 
 class Conv3dDesc(ctypes.Structure):
@@ -75,6 +76,7 @@ SIGNATURES = {
     "mmni_mha_fwd": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp, _vp]),
     "mmni_mha_bwd": (_c_int, [ctypes.POINTER(MhaDesc)] + [_vp] * 11),
     "mmni_mha_mean_probs": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp]),
+    "mmni_mha_dropout_mask": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp]),
     "mmni_conv3d_fwd": (_c_int, [ctypes.POINTER(Conv3dDesc), _vp, _vp, _vp, _vp, _vp]),
     "mmni_conv3d_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Conv3dDesc)]),
     "mmni_conv3d_bwd": (_c_int, [ctypes.POINTER(Conv3dDesc)] + [_vp] * 9),

@@ -604,30 +604,27 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
     if (!bwd) return T * 2 * C * 4 + T * 8 + (size_t)Tsz * NH * 4;
     if (packed)
         return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * (NH == 2 ? 2 : (NH + 3) & ~3) * 4 +
-               (size_t)Tsz * (NH + kDtabPad) * (kDtab32 ? 4 : 8) +
+               (size_t)Tsz * (NH + kDtabPad) * 8 +
                (size_t)NH * 4;
     const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
     return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
 }
 
-// qpl: queries per lane (2 for wattn_fwd_pk2_kernel): a window occupies N / qpl x KS lanes.
+// qpl: queries per lane (2 for wattn_fwd_pk2_kernel, forward only): a window occupies N / qpl x KS lanes.
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
-    const int chunk = packed ? (qpl >= 2 && !(bwd && qpl == 4) ? MMNI_PK2_CHUNK : kPkChunk) : CH;
+    const int chunk = packed ? (qpl >= 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl >= 2 ? (bwd ? (qpl == 4 ? 8 : 4) : MMNI_PK2_KS) : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    int KS = qpl >= 2 ? MMNI_PK2_KS : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (R * KS);
     if (qpl == 2 && !bwd && WPB > MMNI_PK2_FWD_WPB) WPB = MMNI_PK2_FWD_WPB;
-    if (qpl == 4 && !bwd && WPB > MMNI_PK4_FWD_WPB) WPB = MMNI_PK4_FWD_WPB;
     if (WPB < 1) WPB = 1;
-    // the quad backward walks N / 4 bases per slice and stages exactly the window's rows
-    const int NPAD = (bwd && qpl == 4) ? N : (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
+    const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
-    // the quad backward stages the scaled q / dO rows beside K / V (no restage between its passes)
-    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) + (bwd && qpl == 4 ? (size_t)NPAD * 2 * C * 4 : 0);
+    const size_t lds = wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz);
     MMNI_ARG_CHECK(lds <= 160 * 1024, "wattn: LDS footprint %zu B exceeds 160 KiB", lds);
     cfg.KS = KS;
     cfg.WPB = WPB;
@@ -649,27 +646,15 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     return 0;
 }
 
-// Grid of a head-split launch: (window group, head group) items up to the plan's block cap, a
-// multiple of 8 x groups (the kernels deal a group's blocks to one XCD).
-static int head_group_grid(const WAConfig& cfg, int hs) {
-    const int64_t items = (int64_t)cfg.ngroups * hs;
-    int64_t grid = items < cfg.cap ? items : cfg.cap;
-    grid -= grid % (8 * hs);
-    if (grid < 8 * hs) grid = 8 * hs;   // tiny inputs: surplus blocks find no window
-    return (int)grid;
-}
-
 static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
-                    int& qpl, int* hsplit = nullptr) {
+                    int& qpl) {
     const int C = d->C;
     packed = false;
     qpl = 1;
-    if (hsplit) *hsplit = 1;
-    int mf = 0, mb = 0, qf = 1, qb = 1, hb = 1, hf = 1;
-    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, d->wd % 2 == 0 && d->wh % 2 == 0, kf, kb, mf, mb, qf, qb, hb, hf)) {
+    int mf = 0, mb = 0, qf = 1;
+    if (HD == 2 && wattn_pk_kernels(C, d->kind, d->wd * d->wh * d->ww, kf, kb, mf, mb, qf)) {
         maxt = bwd ? mb : mf;
-        qpl = bwd ? qb : qf;
-        if (hsplit) *hsplit = bwd ? hb : hf;
+        qpl = bwd ? 1 : qf;
         packed = true;
         return 0;
     }
@@ -744,18 +729,16 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    int qpl = 1, hs = 1;
-    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl, &hs);
+    int qpl = 1;
+    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
-    MMNI_ARG_CHECK(hs == 1 || (d->heads % hs == 0 && (d->heads / hs) % 2 == 0), "wattn_fwd: head groups");
     WAConfig cfg;
-    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, false, packed, cfg, qpl);
+    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg, qpl);
     if (rc) return rc;
-    if (hs > 1) cfg.grid = head_group_grid(cfg, hs);
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
     a.vmax = packed ? vmax : nullptr;   // the packed kernels fold max|v| into their K/V staging
-    a.hsplit = hs;
+    a.hsplit = 1;
     rc = ensure_lds_attr(kf, cfg.lds);
     if (rc) return rc;
     void* args[] = {&a};
@@ -805,33 +788,18 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     void *kf, *kb;
     int maxt;
     bool packed = false;
-    int qpl = 1, hs = 1;
-    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl, &hs);
+    int qpl = 1;
+    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
-    MMNI_ARG_CHECK(hs == 1 || (d->heads % hs == 0 && (d->heads / hs) % 2 == 0), "wattn_bwd: head groups");
     WAConfig cfg;
-    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, true, packed, cfg, qpl);
+    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg, qpl);
     if (rc) return rc;
-    a.hsplit = hs;
-    if (hs > 1) cfg.grid = head_group_grid(cfg, hs);
-    MMNI_ARG_CHECK(qpl == 1 || cfg.WPB == 1, "wattn_bwd: multi-row kernels need one window per block");
-    MMNI_ARG_CHECK(qpl == 1 || cfg.threads >= (a.g.N / qpl) * cfg.KS, "wattn_bwd: multi-row kernel launch shape");
-    MMNI_ARG_CHECK(qpl != 4 || (a.g.N % 4 == 0 && a.g.wd % 2 == 0 && a.g.wh % 2 == 0 && cfg.KS == 8 && hs == 3),
-                   "wattn_bwd: quad kernel geometry");
+    a.hsplit = 1;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;
     a.dtab_fix = reinterpret_cast<unsigned long long*>(workspace);
     a.fix_shift = 0;
-    if (packed && kDtab32) {
-        // contributions to one table entry per head and block: at most one per query of each window
-        // the block handles; each is < 2^(30 - shift) after scaling, so the 32-bit sum needs
-        // 2^shift >= windows_per_block * N / 2
-        const int64_t per_block = (int64_t)((cfg.ngroups + cfg.grid - 1) / cfg.grid) * cfg.WPB * a.g.N;
-        int sh = 0;
-        while ((int64_t(1) << (sh + 1)) < per_block) ++sh;
-        a.fix_shift = sh;
-    }
     rc = ensure_lds_attr(kb, cfg.lds);
     if (rc) return rc;
     const int ntab = a.g.Tsz * d->heads;

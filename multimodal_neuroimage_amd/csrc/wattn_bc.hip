@@ -10,9 +10,8 @@
 // is the bare recompute + gradient on packed fp32: no online reductions, no cross-lane traffic.
 //
 // LDS facts that shape it (measured here, gfx950): a same-address ds_read_b128 does NOT broadcast
-// (it ran ~16x slower than an 8-byte broadcast), so broadcast rows are stored as separate 8-byte
-// component arrays more than 2040 B apart (out of ds_read2_b64's offset reach), and every
-// component is one ds_read_b64.  The window is a compile-time shape (6^3 at the C3 geometry), so
+// (it ran ~16x slower than 8-byte broadcasts), so broadcast rows are stored as 8-byte component
+// arrays ([component][row] f2) read by ds_read_b64 / ds_read2_b64.  The window is a compile-time shape (6^3 at the C3 geometry), so
 // the key/query coordinates and codes are scalar loop counters, and every table access of a step
 // is one address register plus immediate offsets.
 //
@@ -75,9 +74,13 @@ __device__ __forceinline__ Items items(int NHG) {
 }
 
 constexpr int kThreads = 128;   // two waves: N / 2 <= 128 row pairs
-// f2 stride between the broadcast component arrays: > 255 f2 (2040 B, the reach of ds_read2_b64's
-// offsets), so the compiler keeps every component its own ds_read_b64
-constexpr int kSA = 264;
+
+// Lane -> row-pair map of 6^3 windows.  A lane's table entries at one step are code(t) + const,
+// and 8-byte LDS accesses conflict on (code mod 32) within 32-lane halves (ds_read_b64) and on
+// (code mod 16) within 16-lane groups (ds_read2_b64, which the compiler forms from two steps).
+// With code = 121 z + 11 y + x the identity order collides 2-way in every half; this order
+// (a search over the 108 row pairs) leaves one 2-way collision in one group.
+__constant__ unsigned char kPerm666[108] = {7, 12, 16, 26, 30, 32, 38, 40, 48, 63, 81, 82, 83, 91, 92, 101, 4, 29, 35, 43, 44, 51, 65, 66, 69, 77, 79, 85, 87, 89, 95, 97, 0, 1, 5, 6, 9, 10, 15, 31, 53, 56, 61, 62, 68, 78, 90, 103, 3, 13, 21, 33, 34, 46, 49, 58, 59, 67, 75, 88, 93, 100, 102, 106, 8, 14, 17, 18, 22, 28, 39, 41, 42, 45, 47, 52, 72, 76, 80, 86, 2, 20, 23, 24, 27, 36, 50, 54, 57, 71, 74, 84, 94, 98, 104, 107, 11, 19, 25, 37, 55, 60, 64, 70, 73, 96, 99, 105};
 
 // compile-time window (WD even): tokens t = (i*WH + j)*WW + k, relative codes
 // code = i*TW + j*TH + k, table rows TSZ, the second half starts DC codes later
@@ -88,6 +91,7 @@ struct Win {
     static constexpr int OFF = (WD - 1) * TW + (WH - 1) * TH + (WW - 1);
     static constexpr int DC = (WD / 2) * TW;
     static_assert(WD % 2 == 0, "pairing needs whole planes");
+    static_assert(WD == 6 && WH == 6 && WW == 6, "lane order kPerm666 is for 6^3 windows");
 };
 
 // Per-window shift-region state.  A window spans several regions only if it is the last one
@@ -139,6 +143,27 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
     // lane address of entry (cq - code(n) - DC) = E- for code(n) = 0; E0 / E+ at +DC / +2 DC entries
     const uint32_t lane_base = (uint32_t)((cq - Wn::DC) * EB);
     const f2* kv2 = reinterpret_cast<const f2*>(kv_s);
+    // Software pipeline: the broadcast K/V rows and the (read-only) bias entries of key n + 1 are
+    // loaded during key n.  The private-table read-modify-write is the one ordered access: lanes
+    // share entries across consecutive keys (lane t at key n + 1 reads what lane t - 1 wrote at
+    // key n), a cross-lane order the compiler cannot see, so a compiler barrier after each key's
+    // table stores keeps every later table read behind them (LDS executes a wave's accesses in
+    // order; no wait is needed).
+    f2 kk[2][2], vv[2][2], tbm, tb0, tbp;
+    auto fetch = [&](int nn, int code, f2 (&k_)[2][2], f2 (&v_)[2][2], f2& m_, f2& z_, f2& p_) {
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                k_[v][c] = kv2[(v * 4 + c) * Wn::H + nn];
+                v_[v][c] = kv2[(v * 4 + 2 + c) * Wn::H + nn];
+            }
+        const char* pm = tb + (lane_base - (uint32_t)(code * EB));
+        m_ = *reinterpret_cast<const f2*>(pm);
+        z_ = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
+        p_ = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
+    };
+    fetch(0, 0, kk, vv, tbm, tb0, tbp);
     int n = 0;
     for (int i = 0; i < WD / 2; ++i) {
         for (int j = 0; j < WH; ++j) {
@@ -146,17 +171,19 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
             for (int k = 0; k < WW; ++k, ++n) {
                 const int code = i * Wn::TW + j * Wn::TH + k;
                 char* pm = tb + (lane_base - (uint32_t)(code * EB));   // entry E-  (query t, key n + H)
-                f2 kk[2][2], vv[2][2];
-#pragma unroll
-                for (int v = 0; v < 2; ++v)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        kk[v][c] = kv2[(v * 4 + c) * bc::kSA + n];
-                        vv[v][c] = kv2[(v * 4 + 2 + c) * bc::kSA + n];
-                    }
-                const f2 tbm = *reinterpret_cast<const f2*>(pm);
-                const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
-                const f2 tbp = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
+                // next key's rows and bias entries (the last fetch of the loop reads valid, unused data)
+                const int k1 = k + 1 < WW ? k + 1 : 0;
+                const int j1 = k + 1 < WW ? j : (j + 1 < WH ? j + 1 : 0);
+                const int i1 = (k + 1 < WW || j + 1 < WH) ? i : i + 1;
+                const int n1 = n + 1 < Wn::H ? n + 1 : n;
+                const int code1 = n + 1 < Wn::H ? i1 * Wn::TW + j1 * Wn::TH + k1 : code;
+                f2 nk[2][2], nv[2][2], nm, nz, np;
+                fetch(n1, code1, nk, nv, nm, nz, np);
+                // this key's table-gradient entries (after the previous key's stores)
+                f2* dm = reinterpret_cast<f2*>(pm + DTO);
+                f2* d0 = reinterpret_cast<f2*>(pm + Wn::DC * EB + DTO);
+                f2* dp = reinterpret_cast<f2*>(pm + 2 * Wn::DC * EB + DTO);
+                const f2 om = *dm, o0 = *d0, op = *dp;
                 int rk[2] = {0, 0};
                 if (MASKED) {
                     rk[0] = bc::region_code(reg, i, j, k);
@@ -180,17 +207,18 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
                         dq[u].x[1] = bc::pfma(ds[u][v], kk[v][1], dq[u].x[1]);
                     }
                 }
-                // private table: plain read-modify-write (no two lanes of the wave share an entry
-                // at one step).  Lanes DO share entries across consecutive steps (lane t at key n + 1
-                // reads what lane t - 1 wrote at key n), a cross-lane order the compiler cannot see:
-                // the accesses are volatile so no read moves above an earlier step's write.
-                volatile f2* dm = reinterpret_cast<volatile f2*>(pm + DTO);
-                volatile f2* d0 = reinterpret_cast<volatile f2*>(pm + Wn::DC * EB + DTO);
-                volatile f2* dp = reinterpret_cast<volatile f2*>(pm + 2 * Wn::DC * EB + DTO);
-                const f2 om = *dm, o0 = *d0, op = *dp;
+                // private table: no two lanes of the wave share an entry at one key
                 *d0 = o0 + (ds[0][0] + ds[1][1]);
                 *dm = om + ds[0][1];
                 *dp = op + ds[1][0];
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) { kk[v][c] = nk[v][c]; vv[v][c] = nv[v][c]; }
+                tbm = nm;
+                tb0 = nz;
+                tbp = np;
             }
         }
     }
@@ -209,7 +237,7 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
     const bc::Items it = bc::items(NHG);
     const int tid = threadIdx.x, wave = tid >> 6;
     const bool lane_ok = tid < H;
-    const int t = lane_ok ? tid : 0;
+    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
     for (int e = tid; e < TSZ * 2; e += blockDim.x) {
         tabdt[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
         tabdt[TSZ * 2 + e] = 0.f;
@@ -241,11 +269,11 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
                 q[u].x[1] *= qscale;
                 ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
                 lse2[u] = (f2){a.lse[ti.row * NHT + 2 * it.hp], a.lse[ti.row * NHT + 2 * it.hp + 1]} * kLog2e;
-                f2* kv2 = reinterpret_cast<f2*>(kv_s) + u * 4 * bc::kSA + t;
+                f2* kv2 = reinterpret_cast<f2*>(kv_s) + u * 4 * Wn::H + t;
                 kv2[0] = (f2){kr.x, kr.z};
-                kv2[bc::kSA] = (f2){kr.y, kr.w};
-                kv2[2 * bc::kSA] = (f2){vr.x, vr.z};
-                kv2[3 * bc::kSA] = (f2){vr.y, vr.w};
+                kv2[Wn::H] = (f2){kr.y, kr.w};
+                kv2[2 * Wn::H] = (f2){vr.x, vr.z};
+                kv2[3 * Wn::H] = (f2){vr.y, vr.w};
                 dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
             }
         }
@@ -298,13 +326,13 @@ __device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2]
                 f2 qq[2][2], gg[2][2], ls[2], nd[2];
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
-                    const f2* src = rs2 + u * 6 * bc::kSA + n;
+                    const f2* src = rs2 + u * 6 * Wn::H + n;
                     qq[u][0] = src[0];
-                    qq[u][1] = src[bc::kSA];
-                    gg[u][0] = src[2 * bc::kSA];
-                    gg[u][1] = src[3 * bc::kSA];
-                    ls[u] = src[4 * bc::kSA];
-                    nd[u] = src[5 * bc::kSA];
+                    qq[u][1] = src[Wn::H];
+                    gg[u][0] = src[2 * Wn::H];
+                    gg[u][1] = src[3 * Wn::H];
+                    ls[u] = src[4 * Wn::H];
+                    nd[u] = src[5 * Wn::H];
                 }
                 const f2 tbm = *reinterpret_cast<const f2*>(pm);
                 const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
@@ -351,7 +379,7 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
     const bc::Items it = bc::items(NHG);
     const int tid = threadIdx.x;
     const bool lane_ok = tid < H;
-    const int t = lane_ok ? tid : 0;
+    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
     for (int e = tid; e < TSZ * 2; e += blockDim.x) tab_s[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
     const int coff = it.hp * 4;
     const float qs2 = a.scale * kLog2e;
@@ -376,14 +404,14 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
                 const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti.row * a.os + coff);
                 const float4 orow = *reinterpret_cast<const float4*>(a.o + ti.row * a.os + coff);
                 const float l0 = a.lse[ti.row * NHT + 2 * it.hp], l1 = a.lse[ti.row * NHT + 2 * it.hp + 1];
-                f2* dst = reinterpret_cast<f2*>(rs_s) + u * 6 * bc::kSA + t;
+                f2* dst = reinterpret_cast<f2*>(rs_s) + u * 6 * Wn::H + t;
                 const float d0 = orow.x * gr.x + orow.y * gr.y, d1 = orow.z * gr.z + orow.w * gr.w;
                 dst[0] = (f2){qr.x * qs2, qr.z * qs2};
-                dst[bc::kSA] = (f2){qr.y * qs2, qr.w * qs2};
-                dst[2 * bc::kSA] = (f2){gr.x, gr.z};
-                dst[3 * bc::kSA] = (f2){gr.y, gr.w};
-                dst[4 * bc::kSA] = (f2){l0 * kLog2e, l1 * kLog2e};
-                dst[5 * bc::kSA] = (f2){-d0, -d1};
+                dst[Wn::H] = (f2){qr.y * qs2, qr.w * qs2};
+                dst[2 * Wn::H] = (f2){gr.x, gr.z};
+                dst[3 * Wn::H] = (f2){gr.y, gr.w};
+                dst[4 * Wn::H] = (f2){l0 * kLog2e, l1 * kLog2e};
+                dst[5 * Wn::H] = (f2){-d0, -d1};
             }
         }
         __syncthreads();
@@ -414,12 +442,14 @@ bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind) {
     return g.wd == 6 && g.wh == 6 && g.ww == 6;
 }
 
-static size_t bcA_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 6 * 4 + (size_t)8 * bc::kSA * 8; }
-static size_t bcB_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)12 * bc::kSA * 8; }
+static size_t bcA_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 6 * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8; }
+static size_t bcB_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)12 * bc::Win<6, 6, 6>::H * 8; }
 
-static int bc_blocks(size_t lds, int NHG) {
+// persistent grid: resident workgroups per CU from the LDS footprint and the register budget
+// (waves_per_eu of the kernel: 2-wave workgroups, 4 SIMDs), a multiple of 8 * NHG
+static int bc_blocks(size_t lds, int NHG, int waves_per_eu) {
     int per_cu = (int)((160 * 1024) / lds);
-    if (per_cu > 16) per_cu = 16;
+    if (per_cu > 2 * waves_per_eu) per_cu = 2 * waves_per_eu;
     if (per_cu < 1) per_cu = 1;
     int grid = kNumCU * per_cu;
     grid -= grid % (8 * NHG);
@@ -427,7 +457,7 @@ static int bc_blocks(size_t lds, int NHG) {
 }
 
 size_t wattn_bc_workspace_bytes(const WGeom& g, int heads) {
-    const int gridA = bc_blocks(bcA_lds(), heads / 2);
+    const int gridA = bc_blocks(bcA_lds(), heads / 2, 2);
     return ((size_t)gridA + 1) * g.Tsz * heads * sizeof(float);
 }
 
@@ -448,7 +478,7 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     const int NHG = heads / 2;
     a.hsplit = NHG;
     const size_t ldsA = bcA_lds(), ldsB = bcB_lds();
-    const int gridA = bc_blocks(ldsA, NHG), gridB = bc_blocks(ldsB, NHG);
+    const int gridA = bc_blocks(ldsA, NHG, 2), gridB = bc_blocks(ldsB, NHG, 3);
     const void* kA = reinterpret_cast<const void*>(&wattn_bwdA_bc_kernel<6, 6, 6>);
     const void* kB = reinterpret_cast<const void*>(&wattn_bwdB_bc_kernel<6, 6, 6>);
     int rc = set_lds_limit(kA, ldsA);

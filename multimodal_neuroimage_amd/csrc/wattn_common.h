@@ -72,9 +72,9 @@ struct WAArgs {
     float* dtau;
     unsigned long long* dtab_fix;   // global int64 fixed-point accumulator (workspace)
     unsigned int* maxbits;          // workspace tail: max|dout|, max|v| bits (fixed-point scale)
-    int fix_shift;                  // bits the block-local fixed-point scale is lowered by (32-bit LDS sums)
+    int fix_shift;                  // bits the fixed-point scale is lowered by (0: every kernel here)
     unsigned int* vmax;             // forward (packed kernels): running max|v| (float bits), or null
-    int hsplit;                     // two-row backward: head groups per window (blocks split the heads)
+    int hsplit;                     // head groups per window (blocks split the heads; row-broadcast bwd: head pairs)
 };
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
@@ -89,17 +89,8 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_TAB_SWZ
 #define MMNI_TAB_SWZ 1
 #endif
-#ifndef MMNI_FWD_QPL
-#define MMNI_FWD_QPL 2        // queries per lane of the packed C = 12 forward (4: head-pair blocks only)
-#endif
 #ifndef MMNI_PK2_CHUNK
 #define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
-#endif
-#ifndef MMNI_BWD_QPL
-#define MMNI_BWD_QPL 2        // rows per lane of the packed C = 12 backward (kind 0): 2, or 4 (quads; wd, wh even)
-#endif
-#ifndef MMNI_PK4_FWD_WPB
-#define MMNI_PK4_FWD_WPB 4    // windows per block of the four-query forward (MMNI_FWD_QPL 4)
 #endif
 #ifndef MMNI_PK2_KS
 #define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
@@ -107,33 +98,12 @@ constexpr int CH = 4;                       // keys per online-softmax chunk (ge
 #ifndef MMNI_PK2_FWD_WPB
 #define MMNI_PK2_FWD_WPB 2    // windows per block of the two-query forward: two blocks share a CU
 #endif
-#ifndef MMNI_BWD_HSPLIT
-#define MMNI_BWD_HSPLIT 3     // two-row backward: blocks per window, one per head pair (1: all heads)
-#endif
-#ifndef MMNI_HS_XCD
-#define MMNI_HS_XCD 1         // head-group blocks of a window on one XCD
-#endif
-#ifndef MMNI_FWD_HSPLIT
-#define MMNI_FWD_HSPLIT 1     // two-query forward head groups (3 measured 1.86 vs 1.66 ms: kept at 1)
-#endif
-#ifndef MMNI_PK2_PAIRK
-#define MMNI_PK2_PAIRK 1      // two-row backward: keys j and j + N/2 together (shared table row)
-#endif
-#ifndef MMNI_PK2_KVLDS
-#define MMNI_PK2_KVLDS 1      // two-row backward: pass B's K/V rows read from the pass A staging
-#endif
-#ifndef MMNI_DTAB32
-#define MMNI_DTAB32 0
-#endif
 constexpr int kDtabPad = MMNI_DTAB_PAD;   // packed bwd: table-gradient row stride NH + pad (u64)
 constexpr int kTabSwz = MMNI_TAB_SWZ;     // packed bwd: float4 chunks of table row r XOR-ed with (r >> 3)
-constexpr bool kDtab32 = MMNI_DTAB32;     // packed bwd: 32-bit block-local table-gradient sums
 constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
-// hs_b / hs_f: head groups of the backward / forward kernel (> 1: each block takes C / hs channels).
-int wattn_pk_kernels(int C, int kind, int N, bool quad, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f,
-                     int& qpl_b, int& hs_b, int& hs_f);
+int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f);
 
 // Row-broadcast head_dim-2 backward (wattn_bc.hip): kind 0, head pairs, paired rows t, t + N/2.
 bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind);

@@ -238,40 +238,50 @@ def relative_index(geom, device):
 # ----------------------------------------------------------------------------------------
 # crossmodal multi-head attention core
 # ----------------------------------------------------------------------------------------
-def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_):
+def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_, dropout=0.0, seed=0):
     d = _lib.MhaDesc()
     d.Tq, d.Tk, d.B, d.heads, d.head_dim = Tq, Tk, B, heads, hd
     d.causal_diag = int(causal_diag)
     d.scale = float(scale)
     d.q_stride, d.k_stride, d.v_stride, d.o_stride = int(qs), int(ks), int(vs), int(os_)
+    d.dropout = float(dropout)
+    d.seed = int(seed) & 0xffffffff
     return d
 
 
+def dropout_seed():
+    """A 32-bit seed for one attention-dropout mask, drawn from torch's default CPU generator (so
+    torch.manual_seed makes runs reproducible, as the reference's F.dropout is)."""
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
 class _MHA(torch.autograd.Function):
-    """q (Tq, B, E), k/v (Tk, B, E) dense time-major tensors -> out (Tq, B, E), lse (B, h, Tq)."""
+    """q (Tq, B, E), k/v (Tk, B, E) dense time-major tensors -> out (Tq, B, E), lse (B, h, Tq).
+    dropout p > 0 applies the counter-based mask of `seed` to the probabilities (the backward
+    regenerates it)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, heads, causal_diag, scale):
+    def forward(ctx, q, k, v, heads, causal_diag, scale, dropout, seed):
         require_device(q, k, v, what="mha")
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         Tq, B, E = q.shape
         Tk = k.shape[0]
         out = torch.empty((Tq, B, E), device=q.device, dtype=torch.float32)
         lse = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
         ev = KernelTimer.start()
         check(_lib.load().mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse),
                                         stream_handle(q.device)), "mmni_mha_fwd")
         KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
         ctx.save_for_backward(q, k, v, out, lse)
-        ctx.cfg = (heads, causal_diag, scale)
+        ctx.cfg = (heads, causal_diag, scale, dropout, seed)
         ctx.mark_non_differentiable(lse)
         return out, lse
 
     @staticmethod
     def backward(ctx, dout, _dlse):
         q, k, v, out, lse = ctx.saved_tensors
-        heads, causal_diag, scale = ctx.cfg
+        heads, causal_diag, scale, dropout, seed = ctx.cfg
         Tq, B, E = q.shape
         Tk = k.shape[0]
         dout = dout.contiguous()
@@ -279,28 +289,30 @@ class _MHA(torch.autograd.Function):
         dk = torch.empty_like(k)
         dv = torch.empty_like(v)
         ws = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
         ev = KernelTimer.start()
         check(_lib.load().mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
                                         ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
               "mmni_mha_bwd")
         KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
-        return dq, dk, dv, None, None, None
+        return dq, dk, dv, None, None, None, None, None
 
 
-def mha_core(q, k, v, heads, causal_diag=0, scale=None):
-    """softmax(q*scale @ k^T + causal) @ v over (T, B, E) time-major tensors.
+def mha_core(q, k, v, heads, causal_diag=0, scale=None, dropout=0.0, seed=None):
+    """dropout(softmax(q*scale @ k^T + causal)) @ v over (T, B, E) time-major tensors.
 
-    Returns (out, lse); lse (B, heads, Tq) feeds mha_mean_probs.
-    """
+    Returns (out, lse); lse (B, heads, Tq) feeds mha_mean_probs.  With dropout > 0 the mask comes
+    from `seed` (drawn with dropout_seed() when None); pass the same seed to mha_mean_probs."""
     E = q.shape[-1]
     if scale is None:
         scale = (E // heads) ** -0.5
-    return _MHA.apply(q, k, v, heads, causal_diag, scale)
+    if dropout > 0 and seed is None:
+        seed = dropout_seed()
+    return _MHA.apply(q, k, v, heads, causal_diag, scale, float(dropout), int(seed or 0))
 
 
-def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None):
-    """Head-averaged attention weights (B, Tq, Tk) (multihead_attention.py:131-133)."""
+def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None, dropout=0.0, seed=0):
+    """Head-averaged (dropped) attention weights (B, Tq, Tk) (multihead_attention.py:123,131-133)."""
     Tq, B, E = q.shape
     Tk = k.shape[0]
     if scale is None:
@@ -312,10 +324,18 @@ def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None):
     if k.stride(1) != E or k.stride(0) != B * E:
         k = k.contiguous()
     probs = torch.empty((B, Tq, Tk), device=q.device, dtype=torch.float32)
-    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E)
+    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
     check(_lib.load().mmni_mha_mean_probs(d, ptr(q), ptr(k), ptr(lse), ptr(probs), stream_handle(q.device)),
           "mmni_mha_mean_probs")
     return probs
+
+
+def mha_dropout_mask(Tq, Tk, B, heads, dropout, seed, device, causal_diag=0):
+    """(B, heads, Tq, Tk) multipliers (0 or 1/(1-p)) of the kernels' dropout mask for `seed`."""
+    mask = torch.empty((B, heads, Tq, Tk), device=device, dtype=torch.float32)
+    d = _mha_desc(Tq, Tk, B, heads, 1, causal_diag, 1.0, heads, heads, heads, heads, dropout, seed)
+    check(_lib.load().mmni_mha_dropout_mask(d, ptr(mask), stream_handle(device)), "mmni_mha_dropout_mask")
+    return mask
 
 
 # ----------------------------------------------------------------------------------------

@@ -6,14 +6,18 @@ bmm -> mask -> fp32 softmax -> bmm core (multihead_attention.py:109-130) is one 
 HIP kernel (libmmni.so mmni_mha_fwd/bwd) reading the time-major (T, B, E) projections in place.
 The head-averaged weights (second return value) are produced by a separate kernel only when
 asked for (need_weights=True, the reference's behaviour); TransformerEncoderLayer discards
-them, so the encoder never materialises a T x T tensor.
+them, so the encoder never materialises a T x T tensor.  Attention dropout (the reference's
+F.dropout of the probabilities, multihead_attention.py:123; default --attn_dropout 0.1,
+main.py:176) runs inside the kernels from a counter-based mask: one seed per call, drawn from
+torch's default generator, regenerated in the backward.  The weights are not differentiable
+(no caller of the reference back-propagates through them).
 """
 import torch
 from torch import nn
 from torch.nn import Parameter
 import torch.nn.functional as F
 
-from ..functional import mha_core, mha_mean_probs
+from ..functional import dropout_seed, mha_core, mha_mean_probs
 
 
 def causal_diag_of(attn_mask, Tq, Tk):
@@ -72,9 +76,6 @@ class MultiheadAttention(nn.Module):
         if self.bias_k is not None or self.add_zero_attn:
             raise NotImplementedError("add_bias_kv / add_zero_attn are not used by the reference callers and are "
                                       "not implemented by the fused kernel")
-        if self.training and self.attn_dropout > 0:
-            raise NotImplementedError("MultiheadAttention: attention dropout > 0 in training is not implemented by "
-                                      "the fused kernel; construct with attn_dropout=0")
         tgt_len, bsz, embed_dim = query.size()
         assert embed_dim == self.embed_dim
         assert key.size() == value.size()
@@ -89,11 +90,13 @@ class MultiheadAttention(nn.Module):
             q = self._in_proj(query, end=self.embed_dim)
             k = self._in_proj(key, start=self.embed_dim, end=2 * self.embed_dim)
             v = self._in_proj(value, start=2 * self.embed_dim)
-        attn, lse = mha_core(q, k, v, self.num_heads_mult, diag, self.scaling)
+        p = float(self.attn_dropout) if self.training else 0.0
+        seed = dropout_seed() if p > 0 else 0
+        attn, lse = mha_core(q, k, v, self.num_heads_mult, diag, self.scaling, dropout=p, seed=seed)
         attn = self.out_proj(attn)
         weights = None
         if need_weights:
-            weights = mha_mean_probs(q, k, lse, self.num_heads_mult, diag, self.scaling)
+            weights = mha_mean_probs(q, k, lse, self.num_heads_mult, diag, self.scaling, dropout=p, seed=seed)
         return attn, weights
 
     def in_proj_qkv(self, query):

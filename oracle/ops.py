@@ -99,9 +99,11 @@ def causal_diag(Tq, Tk):
     return 1 + abs(Tk - Tq)
 
 
-def mha_core(q, k, v, heads, diag=0, scale=None):
-    """bmm / fp32 softmax / bmm core of MultiheadAttention.forward (multihead_attention.py:92-133)
-    on time-major (T, B, E) tensors.  Returns (out (Tq,B,E), head-mean weights (B,Tq,Tk))."""
+def mha_core(q, k, v, heads, diag=0, scale=None, drop_mask=None):
+    """bmm / fp32 softmax / dropout / bmm core of MultiheadAttention.forward
+    (multihead_attention.py:92-133) on time-major (T, B, E) tensors.  drop_mask (B, heads, Tq, Tk):
+    the multipliers F.dropout applied to the probabilities (:123), None for no dropout.
+    Returns (out (Tq,B,E), head-mean (dropped) weights (B,Tq,Tk))."""
     Tq, B, E = q.shape
     Tk = k.shape[0]
     hd = E // heads
@@ -115,6 +117,8 @@ def mha_core(q, k, v, heads, diag=0, scale=None):
         mask = torch.triu(torch.full((Tq, Tk), float("-inf"), dtype=w.dtype, device=w.device), diag)
         w = w + mask.unsqueeze(0)
     w = torch.softmax(w, dim=-1)
+    if drop_mask is not None:
+        w = w * drop_mask.reshape(B * heads, Tq, Tk).to(w.dtype)
     out = torch.bmm(w, vh).transpose(0, 1).reshape(Tq, B, E)
     mean_w = w.view(B, heads, Tq, Tk).sum(dim=1) / heads
     return out, mean_w

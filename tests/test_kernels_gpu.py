@@ -520,3 +520,91 @@ def test_window_attention_grads_are_deterministic(device, cross):
     for r in res[1:]:
         for a, b in zip(r, res[0]):
             assert torch.equal(a, b)
+
+
+MHA_DROP = [
+    # Tq, Tk, B, heads, hd, causal, p
+    (64, 64, 2, 4, 7, True, 0.1),
+    (130, 100, 1, 3, 14, True, 0.3),
+    (50, 70, 2, 12, 8, False, 0.5),
+    (368, 368, 2, 12, 7, True, 0.1),
+]
+
+
+@pytest.mark.parametrize("Tq,Tk,B,heads,hd,causal,p", MHA_DROP)
+def test_mha_dropout_vs_oracle_with_the_kernel_mask(device, Tq, Tk, B, heads, hd, causal, p):
+    """Attention dropout (multihead_attention.py:123): the forward, the head-mean weights and all
+    three gradients equal the fp64 oracle run with the very mask the kernels regenerate from the
+    seed (exported by mmni_mha_dropout_mask), so forward and backward apply one mask."""
+    gen = torch.Generator().manual_seed(Tq + 7 * Tk + hd)
+    E = heads * hd
+    q, k, v = [torch.randn(T, B, E, generator=gen, dtype=torch.float64) for T in (Tq, Tk, Tk)]
+    gout = torch.randn(Tq, B, E, generator=gen, dtype=torch.float64)
+    diag = O.causal_diag(Tq, Tk) if causal else 0
+    seed = 1234 + Tq
+    mask = MF.mha_dropout_mask(Tq, Tk, B, heads, p, seed, device)
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    ref, ref_w = O.mha_core(*leaves, heads, diag, drop_mask=mask.double().cpu())
+    (ref * gout).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (q, k, v)]
+    out, lse = MF.mha_core(*dev, heads, diag, dropout=p, seed=seed)
+    (out * gout.float().to(device)).sum().backward()
+    w = MF.mha_mean_probs(dev[0], dev[1], lse, heads, diag, dropout=p, seed=seed)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL
+    assert rel_err(w, ref_w) < TOL
+    for a, b in zip(dev, leaves):
+        assert rel_err(a.grad, b.grad) < TOL
+
+
+def test_mha_dropout_mask_statistics(device):
+    """Keep rate 1 - p and unbiased multipliers (E[mask] = 1) within 5 sigma; masks differ across
+    seeds, heads and rows; p = 0 is the no-dropout path bit for bit."""
+    B, H, T, p = 2, 12, 368, 0.1
+    m = MF.mha_dropout_mask(T, T, B, H, p, 99, device)
+    n = m.numel()
+    keep = float((m > 0).float().mean())
+    sigma = (p * (1 - p) / n) ** 0.5
+    assert abs(keep - (1 - p)) < 5 * sigma
+    assert abs(float(m.double().mean()) - 1.0) < 5 * sigma / (1 - p)
+    vals = torch.unique(m).tolist()
+    assert len(vals) == 2 and vals[0] == 0.0 and abs(vals[1] - 1 / (1 - p)) < 1e-6
+    m2 = MF.mha_dropout_mask(T, T, B, H, p, 100, device)
+    assert not torch.equal(m, m2)
+    assert not torch.equal(m[0, 0], m[0, 1]) and not torch.equal(m[0, 0, 0], m[0, 0, 1])
+    # per-column keep rates stay near 1 - p (no column bias from the per-row hash)
+    col = (m > 0).float().mean(dim=(0, 1, 2))
+    assert float((col - (1 - p)).abs().max()) < 6 * (p * (1 - p) / (B * H * T)) ** 0.5
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(T, B, H * 7, device=device) for _ in range(3))
+    o0, _ = MF.mha_core(q, k, v, H, 1)
+    o1, _ = MF.mha_core(q, k, v, H, 1, dropout=0.0, seed=5)
+    assert torch.equal(o0, o1)
+
+
+def test_crossmodal_model_trains_with_reference_dropout_defaults(device):
+    """Transformer_Net_Cross_Attention with the reference's default dropouts (--attn_dropout 0.1
+    etc., main.py:176-195) runs a training step (train mode, dropout in the kernels) and its eval
+    forward equals the dropout-free path."""
+    from multimodal_neuroimage_amd import model as M
+    kw = dict(fine_tune_task="binary_classification", intermediate_vec=84, num_heads_mult=12, nlevels=2,
+              attn_dropout=0.1, attn_dropout_u=0.1, relu_dropout=0.1, res_dropout=0.1, embed_dropout=0.1,
+              out_dropout=0.0, attn_mask=True, sequence_length=368, feature_map_gen="convolution_ul+l",
+              feature_map_size="same", mixing="U2L_and_L2U", concat_method="concat", fmri_type="divided_frequency")
+    torch.manual_seed(0)
+    m = M.Transformer_Net_Cross_Attention(**kw).to(device)
+    xl, xu = torch.randn(2, 368, 84, device=device), torch.randn(2, 368, 84, device=device)
+    m.train()
+    out = m(xl, xu)["binary_classification"]
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out))
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+    m.eval()
+    with torch.no_grad():
+        a = m(xl, xu)["binary_classification"]
+        for mod in m.modules():
+            if hasattr(mod, "attn_dropout"):
+                mod.attn_dropout = 0.0
+        b = m(xl, xu)["binary_classification"]
+    assert torch.equal(a, b)
