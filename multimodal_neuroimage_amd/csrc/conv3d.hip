@@ -348,7 +348,9 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
     float* x_s = dz_s + Tout * COUT;          // [Tin][CIN]
     const int tid = threadIdx.x;
     float acc[MAXP][COUT];
-    float dbs = 0.f;   // db[pl] partial (lanes pl < COUT)
+    float dbl[COUT];   // db partial: sum of the dz rows this thread staged (any COUT vs npairs)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) dbl[co] = 0.f;
 #pragma unroll
     for (int m = 0; m < MAXP; ++m)
 #pragma unroll
@@ -357,7 +359,6 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
     const int G = MAXP == 1 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;   // lane groups over voxels
     const int gi = MAXP == 1 ? tid / npairs : 0;
     const int pl = MAXP == 1 ? tid - gi * npairs : tid;
-    const int plc = pl < COUT ? pl : COUT - 1;
     // x_s offset of each owned pair relative to the voxel's halo base
     int xo[MAXP];
 #pragma unroll
@@ -395,7 +396,10 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
                 for (int co = 0; co < COUT; ++co) g[co] = 0.f;
             }
 #pragma unroll
-            for (int co = 0; co < COUT; ++co) dz_s[e * COUT + co] = g[co];
+            for (int co = 0; co < COUT; ++co) {
+                dz_s[e * COUT + co] = g[co];
+                dbl[co] += g[co];
+            }
         }
         // halo rows as float4 chunks when rows are 16-B multiples: the index math runs per chunk
         const bool vec4 = CIN % 4 == 0 && (Tout * COUT) % 4 == 0 && reinterpret_cast<uintptr_t>(a.x) % 16 == 0;
@@ -432,7 +436,6 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             float g[COUT];
 #pragma unroll
             for (int co = 0; co < COUT; ++co) g[co] = dz_s[u * COUT + co];
-            dbs += dz_s[u * COUT + plc];
 #pragma unroll
             for (int m = 0; m < MAXP; ++m) {
                 const float xv = x_s[hb * CIN + xo[m]];
@@ -446,17 +449,15 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             }
         }
     }
-    // lane groups (MAXP 1, G > 1): sum the G partials of a pair through LDS first, so a block
-    // flushes one atomic per (pair, co) rather than G (same-address atomics serialise in L2)
+    // lane groups (MAXP 1, G > 1): sum the G partials of a pair through LDS in group order, so
+    // the block's partial row is written once per (pair, co)
     bool flush = gi < G;
     if (MAXP == 1 && G > 1) {
         __syncthreads();
-        float* red = smem;                        // [G][npairs][COUT], then [G][COUT] db partials
-        float* redb = red + G * npairs * COUT;
+        float* red = smem;                        // [G][npairs][COUT]
         if (gi < G) {
 #pragma unroll
             for (int co = 0; co < COUT; ++co) red[(gi * npairs + pl) * COUT + co] = acc[0][co];
-            if (pl < COUT) redb[gi * COUT + pl] = dbs;
         }
         __syncthreads();
         if (gi == 0) {
@@ -465,11 +466,6 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
                 float sum = 0.f;
                 for (int q = 0; q < G; ++q) sum += red[(q * npairs + pl) * COUT + co];
                 acc[0][co] = sum;
-            }
-            if (pl < COUT) {
-                float sum = 0.f;
-                for (int q = 0; q < G; ++q) sum += redb[q * COUT + pl];
-                dbs = sum;
             }
         }
         flush = gi == 0;
@@ -486,7 +482,17 @@ __global__ __launch_bounds__(256) void conv3d_dw_kernel(ConvArgs a) {
             for (int co = 0; co < COUT; ++co) row[((int64_t)co * CIN + ci) * K3 + t] = acc[m][co];
         }
     }
-    if (pl < COUT && flush) row[ncw + pl] = dbs;
+    // db: the 256 per-thread sums, reduced in a fixed order by lanes co < COUT
+    __syncthreads();
+    float* redd = smem;   // [COUT][256]
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) redd[co * 256 + tid] = dbl[co];
+    __syncthreads();
+    if (tid < COUT) {
+        float sum = 0.f;
+        for (int q = 0; q < 256; ++q) sum += redd[tid * 256 + q];
+        row[ncw + tid] = sum;
+    }
 }
 
 static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
@@ -534,9 +540,11 @@ static int dw_plan(ConvArgs& a, int& grid, size_t& lds) {
     const int npairs = a.kd * a.kh * a.kw * CIN;
     MMNI_ARG_CHECK(npairs <= 1024, "conv3d_dw: k^3*Cin = %d exceeds 1024 pairs", npairs);
     grid = a.ntiles < kNumCU * MMNI_CONV_DW_BPC ? a.ntiles : kNumCU * MMNI_CONV_DW_BPC;
-    // the group reduction of the MAXP 1 kernel reuses the LDS image: [G][npairs][COUT] + [G][COUT]
+    // the group reduction of the MAXP 1 kernel ([G][npairs][COUT]) and the db reduction
+    // ([COUT][256]) reuse the LDS image
     const int G = npairs <= 256 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;
-    const size_t red = (size_t)G * (npairs + 1) * COUT * 4;
+    size_t red = (size_t)G * npairs * COUT * 4;
+    if (red < (size_t)256 * COUT * 4) red = (size_t)256 * COUT * 4;
     lds = bytes() > red ? bytes() : red;
     MMNI_ARG_CHECK(lds <= 64 * 1024, "conv3d_dw: group reduction exceeds the LDS tile");
     return 0;

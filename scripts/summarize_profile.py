@@ -26,9 +26,9 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk2?_kernel<(\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
-    m = re.search(r"mmni::wattn_bwd_pk2_kernel<(\d+), \d+>", name)   # kind 0 only
-    if m:   # <4, .>: the head-pair split of the C = 12 layer (three blocks per window)
-        return f"wattn_bwd_k0_C{12 if m.group(1) == '4' else m.group(1)}"
+    m = re.search(r"mmni::wattn_bwd[AB]_bc_kernel<6, 6, 6>", name)   # kind 0, C = 12, 6^3 windows
+    if m:   # the row-broadcast backward: pass A + pass B (+ the table-gradient column sum) = one call
+        return "wattn_bwd_k0_C12"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
     if m:
         return f"{m.group(1)}_hd{m.group(2)}"
@@ -92,6 +92,14 @@ def main(tag):
         key = bench_key(name) or name
         f, w = d.get("FETCH_SIZE"), d.get("WRITE_SIZE")
         hbm = (2 * f + w) * 1024 if f is not None and w is not None else None
+        if key in kernels and hbm is not None and kernels[key]["hbm_bytes_per_launch"] is not None:
+            # several kernels make one call (the row-broadcast backward's passes A and B): bytes add
+            k = kernels[key]
+            k["rocprof_name"] += " + " + name
+            k["fetch_kb"] += f
+            k["write_kb"] += w
+            k["hbm_bytes_per_launch"] += hbm
+            continue
         kernels[key] = dict(rocprof_name=name, fetch_kb=f, write_kb=w, hbm_bytes_per_launch=hbm,
                             launches=d.get("launches"))
     json.dump(dict(tag=tag, correction="bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (MI355X_MICROARCH.md §HBM)",

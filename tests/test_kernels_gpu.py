@@ -179,6 +179,9 @@ CONV = [
     (1, (9, 9, 9), 6, 3, (3, 3, 3), (1, 1, 1), (1, 1, 1), 0.2),
     (2, (1, 20, 24), 6, 12, (1, 3, 3), (1, 1, 1), (0, 1, 1), 0.2),
     (2, (1, 84, 84), 1, 12, (1, 7, 7), (1, 7, 7), (0, 0, 0), 1.0),
+    # fewer (tap, Cin) pairs than output channels: db has columns no dW lane owns
+    (1, (12, 12, 12), 1, 12, (2, 2, 2), (2, 2, 2), (0, 0, 0), 1.0),
+    (2, (5, 6, 7), 1, 6, (1, 1, 1), (1, 1, 1), (0, 0, 0), 0.2),
 ]
 
 
