@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 3
+#define MMNI_ABI_VERSION 4
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -113,12 +113,17 @@ int mmni_relative_index(const mmni_wattn_desc* d, int32_t* idx, void* stream);
  *   dropout(softmax_fp32(q*scale @ k^T + mask)) @ v, mask = -inf where (j - i) >= causal_diag
  *   (buffered_future_mask, crossmodal_transformer.py:179-186, causal_diag = 1+|Tk-Tq|).
  * Time-major layout (T, B, E): element (t, b, h, c) at ptr[(t*B + b)*stride + h*head_dim + c].
- * head_dim 1..16 (padded to 4 / 8 / 16 on the f32 MFMA).
+ * head_dim 1..16, padded to 4 / 8 / 16.  The contractions run on the bf16 matrix cores with each
+ * fp32 operand split into bf16 hi + lo and three products (hi*hi + hi*lo + lo*hi) accumulated in
+ * fp32: ~2^-16 relative error per product, fp32-class results.
  * Attention dropout (multihead_attention.py:123, F.dropout of the probabilities): dropout = p in
  * [0, 1); element (b, h, i, j) is kept iff a counter-based hash of (seed, (b*heads + h)*Tq + i, j)
  * falls below (1 - p) * 2^32, and kept probabilities are scaled by 1 / (1 - p).  The same seed in
  * the backward regenerates the same mask.  p = 0 is the exact no-dropout path.  (ABI v3 added
  * dropout and seed.)
+ * Workspaces (ABI v4): >= mmni_mha_{fwd,bwd}_workspace_bytes(d) bytes, 256-byte aligned, contents
+ * ignored; they hold the bf16 split images of the 64-row tiles (written by the call itself) and,
+ * in the backward, delta = rowsum(dO * O).
  * ------------------------------------------------------------------------------------ */
 typedef struct mmni_mha_desc {
     int32_t Tq, Tk, B, heads, head_dim;
@@ -129,13 +134,15 @@ typedef struct mmni_mha_desc {
     uint32_t seed;              /* dropout stream; forward and backward must agree         */
 } mmni_mha_desc;
 
+size_t mmni_mha_fwd_workspace_bytes(const mmni_mha_desc* d);
+size_t mmni_mha_bwd_workspace_bytes(const mmni_mha_desc* d);
 /* out: (Tq, B, E) rows with o_stride; lse: (B, heads, Tq) of the undropped softmax. */
 int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                 float* out, float* lse, void* stream);
-/* dq/dk/dv overwritten; workspace: (B, heads, Tq) floats for delta = rowsum(dO*O). */
+                 float* out, float* lse, void* workspace, void* stream);
+/* dq/dk/dv overwritten. */
 int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
                  const float* out, const float* dout, const float* lse,
-                 float* dq, float* dk, float* dv, float* workspace, void* stream);
+                 float* dq, float* dk, float* dv, void* workspace, void* stream);
 /* Head-averaged (dropped) attention probabilities (B, Tq, Tk) — the second return value of
  * MultiheadAttention.forward (multihead_attention.py:131-133). */
 int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const float* k,

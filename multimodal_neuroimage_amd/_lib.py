@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -73,7 +73,9 @@ SIGNATURES = {
     "mmni_window_rows": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
     "mmni_window_mask": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
     "mmni_relative_index": (_c_int, [ctypes.POINTER(WAttnDesc), _vp, _vp]),
-    "mmni_mha_fwd": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mmni_mha_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MhaDesc)]),
+    "mmni_mha_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MhaDesc)]),
+    "mmni_mha_fwd": (_c_int, [ctypes.POINTER(MhaDesc)] + [_vp] * 7),
     "mmni_mha_bwd": (_c_int, [ctypes.POINTER(MhaDesc)] + [_vp] * 11),
     "mmni_mha_mean_probs": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp, _vp, _vp, _vp]),
     "mmni_mha_dropout_mask": (_c_int, [ctypes.POINTER(MhaDesc), _vp, _vp]),

@@ -10,19 +10,27 @@
 // (t, b, head, c) at ptr[(t*B + b)*stride + head*hd + c] — so the reference's
 // .view(T, B*h, d).transpose(0,1) copies (multihead_attention.py:92-96) never happen.
 //
-// Contractions on the f32 matrix cores (v_mfma_f32_16x16x4_f32; exact fp32, the same 157 TF as
-// the packed VALU, so the VALU stays free for the softmax).  head_dim d is padded to HDP = 4, 8
-// or 16 (7 -> 8, 14 -> 16; padding lanes read zeros).  One wave owns 16 rows; K/V (or Q/dO) tiles
-// of 64 rows are staged in LDS and consumed as 4 sub-tiles of 16.
-//   forward   S^T(16 keys x 16 queries) = K Q^T        (HDP/4 MFMAs per sub-tile)
-//             O^T(d x 16 queries)     += V^T P^T       (4 MFMAs per sub-tile; P^T is the S^T
-//                                                      accumulator itself: C/D rows = keys = the
-//                                                      B operand's k index, no data movement)
+// Contractions on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16) with every fp32 operand split
+// into bf16 hi + lo parts and three products hi*hi + hi*lo + lo*hi accumulated in fp32: relative
+// error ~2^-16 per product, i.e. fp32-class results at 16x the f32 MFMA rate (gfx950 has no xf32).
+// head_dim d is padded to HDP = 4, 8 or 16 (7 -> 8, 14 -> 16).  One wave owns 16 rows; tiles of 64
+// rows of the other operand are staged in LDS as bf16 split images and consumed as 4 sub-tiles:
+//   S-type  (contraction over d)   S^T = K Q^T etc.: the 3 terms are laid along the MFMA's K = 32
+//           (LDS side [hi | hi | lo], register side [hi | lo | hi]); one MFMA per 16 x 16 sub-tile
+//           for d <= 8, two for d = 16.
+//   Z-type  (contraction over rows) O^T += V^T P^T etc.: the fp32 MFMA accumulator of the S-type
+//           product is split in registers and is the B operand as it lies (its rows are the K
+//           index).  d <= 8: rows 0-7 of the A image carry Zh (x [Wh | Wl]) and rows 8-15 Zl
+//           (x [Wh | 0]), one MFMA per 16 rows, halves summed once at the end; d = 16: three MFMAs
+//           per 32 rows.
+//   forward   S^T = K Q^T, O^T += V^T P^T
 //   dq        S^T, dP^T = V dO^T, dS^T, dQ^T += K^T dS^T
 //   dk, dv    S = Q K^T, dP = dO V^T, dS, dV^T += dO^T P, dK^T += Q^T dS
 // Online softmax in the log2 domain: each lane holds 4 keys of one query per sub-tile; the row
-// max is two cross-lane shuffles per 64 keys, the row sum stays a per-lane partial until the end.
-// Causal tiles past a wave's diagonal are skipped.  No atomics: deterministic.
+// max is two cross-lane shuffles per 64 keys.  Without dropout and with d < HDP the softmax
+// denominator rides in the padding row of V (ones), so the MFMA forms it.  The backward folds
+// -lse and -delta into the accumulator initialisation.  Causal tiles past a wave's diagonal are
+// skipped.  No atomics: deterministic.
 //
 // Attention dropout (multihead_attention.py:123, F.dropout on the probabilities, reference default
 // --attn_dropout 0.1, main.py:176): counter-based, keep(b*h, i, j) = hash(seed, (b*h)*Tq + i, j)
@@ -32,10 +40,27 @@
 namespace mmni {
 
 typedef float mf4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ mf4 mfma4(float a, float b, mf4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ mf4 mfma_bf(u4 a, u4 b, mf4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
 }
+
+// bf16 split of fp32: hi = truncation (exact as an fp32), lo = round(x - hi)
+__device__ __forceinline__ float bf_hi(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pk_hi(float a, float b) {   // {hi(a), hi(b)}
+    return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ uint32_t pk_rn(float a, float b) {
+    bf16x2 r;
+    r[0] = (__bf16)a;
+    r[1] = (__bf16)b;
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_lo(float a, float b) { return pk_rn(a - bf_hi(a), b - bf_hi(b)); }
 
 struct MhaArgs {
     int Tq, Tk, B, H, hd, causal;   // causal: diag (<=0 none)
@@ -57,10 +82,33 @@ struct MhaArgs {
     float inv_keep;                 // 1 / (1 - p)
     uint32_t thresh;                // keep iff hash < thresh
     uint32_t seed;
+    int nqt, nkt;                   // 64-row tiles of the query / key sequences
+    // bf16 split images in the workspace (mha_split_kernel), [bh][tile][...]
+    const uint16_t* kx;             // K ext
+    const uint16_t* kz;             // K Z
+    const uint16_t* vx;             // V ext
+    const uint16_t* vz;             // V Z (forward: padding row of ones)
+    const uint16_t* qx;             // Q * scale * log2e ext
+    const uint16_t* qz;             // Q * scale * log2e Z
+    const uint16_t* gx;             // dO ext
+    const uint16_t* gz;             // dO Z
 };
 
 constexpr int MT = 64;      // rows per LDS tile and per workgroup (4 waves x 16)
-constexpr int VST = 20;     // row stride of the tiles read as [row 4g+i][col lane&15] (conflict-free halves)
+
+// LDS image geometry per padded head_dim
+template <int HDP>
+struct Geo {
+    static constexpr int NX = (3 * HDP + 31) / 32;   // S-type MFMAs per 16 x 16 sub-tile
+    static constexpr int XS = 32 * NX + 8;           // ext image row stride (bf16): 80 / 144 B, conflict-free
+    static constexpr bool RS = HDP <= 8;             // Z image: row-split (one MFMA per 16 rows)
+    static constexpr int ZS = RS ? 136 : 72;         // Z image row stride (bf16): 272 / 144 B
+    static constexpr int ZR = RS ? 16 : 32;          // Z image rows (RS: hi 0-7, lo 8-15; else hi 0-15, lo 16-31)
+    static constexpr int EW = 32 * NX;               // ext image row in global (unpadded)
+    static constexpr int ZW = RS ? 128 : 64;         // Z image row in global (unpadded)
+    static constexpr int XT = MT * EW;               // ext tile (bf16 elements)
+    static constexpr int ZT = ZR * ZW;               // Z tile (bf16 elements)
+};
 
 // ---- dropout hash (lowbias32 mixer, two rounds keyed by row then column)
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -85,8 +133,288 @@ __device__ __forceinline__ int key_end(const MhaArgs& a, int i) {
     return e < a.Tk ? e : a.Tk;
 }
 
+// block -> row tile: alternate the two ends of the sequence, so the causal mask's long and
+// short tiles interleave in dispatch order (even load per CU)
+__device__ __forceinline__ int zigzag(int x, int n) { return (x & 1) ? n - 1 - (x >> 1) : (x >> 1); }
+
 __device__ __forceinline__ float load_pad(const float* base, int64_t rowoff, int c, int hd, bool ok) {
     return (ok && c < hd) ? base[rowoff + c] : 0.f;
+}
+
+// ------------------------------------------------------------------------------------
+// split images.  mha_split_kernel writes, once per call, each operand's 64-row tiles as bf16
+// images in the workspace: EXT rows [hi | hi | lo | 0] (the S-type A operand), Z rows (the Z-type
+// A operand, see Geo).  The attention kernels then stage a tile with 16-byte copies.
+// ------------------------------------------------------------------------------------
+struct SplitOp {
+    const float* x;     // (T, B, stride) time-major, head h at column h * hd
+    int64_t xs;         // row stride of (t, b)
+    int T, ntiles;
+    float mul;
+    int ones;           // padding dim that reads 1.0 (-1: none)
+    uint16_t* ext;      // [bh][tile][MT][EW] or null
+    uint16_t* z;        // [bh][tile][ZR][ZW] or null
+};
+struct SplitArgs {
+    SplitOp op[4];
+    int nops;
+    int B, H, hd;
+    // delta = rowsum(dO * O) as the last z-slice (backward): o/g rows with stride os
+    const float* o;
+    const float* g;
+    int64_t os;
+    int Tq;
+    float* delta;       // (B, H, Tq)
+};
+
+// grid (tiles, B * H): a block builds the 64-row tile images of one head for every operand in LDS
+// (all operands' loads in flight together), adds the delta rows of the tile (backward), then
+// writes the images out with coalesced 16-byte stores
+template <int HDP>
+__global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
+    using G = Geo<HDP>;
+    constexpr int IMG = G::XT + G::ZT;
+    __shared__ __attribute__((aligned(16))) uint16_t img[4 * IMG];
+    const int tile = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, hd = sa.hd, H = sa.H;
+    const int b = bh / H, h = bh % H;
+    for (int e = tid; e < sa.nops * IMG / 8; e += 256) reinterpret_cast<u4*>(img)[e] = (u4){0u, 0u, 0u, 0u};
+    constexpr int DP = HDP / 2, NB = 32 * DP;   // 2 x 2 blocks (rows r, r+1; dims d, d+1) per operand
+    constexpr int IT = (4 * NB + 255) / 256;
+    float x[IT][2][2];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        // NB is a multiple of 64: the operand index is wave-uniform
+        const int e = tid + 256 * it, o = __builtin_amdgcn_readfirstlane(e / NB), blk = e - o * NB;
+        const int rp = blk / DP, dp = blk - rp * DP;
+        const bool live = o < sa.nops && tile < sa.op[o < sa.nops ? o : 0].ntiles;
+        const SplitOp& op = sa.op[o < sa.nops ? o : 0];
+        const float* src = op.x + (int64_t)b * op.xs + h * hd;
+        const int64_t rs = (int64_t)sa.B * op.xs;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) {
+                const int j = tile * MT + 2 * rp + rr, c = 2 * dp + dd;
+                float v = 0.f;
+                if (live && j < op.T) v = c < hd ? src[(int64_t)j * rs + c] * op.mul : (c == op.ones ? 1.f : 0.f);
+                x[it][rr][dd] = v;
+            }
+    }
+    float dl = 0.f;   // delta of row tid (backward)
+    const int di = tile * MT + tid;
+    const bool dlive = sa.delta != nullptr && tid < MT && di < sa.Tq;
+    if (dlive) {   // all 2 * hd loads issued together
+        const int64_t off = ((int64_t)di * sa.B + b) * sa.os + h * hd;
+        float ov[HDP], gv[HDP];
+#pragma unroll
+        for (int c = 0; c < HDP; ++c) {
+            ov[c] = c < hd ? sa.o[off + c] : 0.f;
+            gv[c] = c < hd ? sa.g[off + c] : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < HDP; ++c) dl = fmaf(ov[c], gv[c], dl);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = tid + 256 * it, o = __builtin_amdgcn_readfirstlane(e / NB), blk = e - o * NB;
+        if (o >= sa.nops) continue;
+        const SplitOp& op = sa.op[o];
+        if (tile >= op.ntiles) continue;
+        const int rp = blk / DP, dp = blk - rp * DP, r = 2 * rp, d = 2 * dp;
+        uint32_t* xw = reinterpret_cast<uint32_t*>(img + o * IMG);
+        uint32_t* zw = reinterpret_cast<uint32_t*>(img + o * IMG + G::XT);
+        if (op.ext) {
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int w = ((r + rr) * G::EW + d) >> 1;
+                const uint32_t hi = pk_hi(x[it][rr][0], x[it][rr][1]);
+                xw[w] = hi;
+                xw[w + HDP / 2] = hi;
+                xw[w + HDP] = pk_lo(x[it][rr][0], x[it][rr][1]);
+            }
+        }
+        if (op.z) {
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) {
+                const uint32_t hi = pk_hi(x[it][0][dd], x[it][1][dd]), lo = pk_lo(x[it][0][dd], x[it][1][dd]);
+                if (G::RS) {   // [m][st][lg][j]: m < 8 hi (j and j + 4), m >= 8 lo (j < 4)
+                    const int w = ((d + dd) * G::ZW + (r >> 4) * 32 + ((r & 15) >> 2) * 8 + (r & 3)) >> 1;
+                    zw[w] = hi;
+                    zw[w + 2] = hi;
+                    zw[w + 4 * G::ZW] = lo;   // row + 8
+                } else {       // [d][c][lg][j]: hi rows 0-15, lo rows 16-31
+                    const int j = ((r >> 4) & 1) * 4 + (r & 3);
+                    const int w = ((d + dd) * G::ZW + (r >> 5) * 32 + ((r & 15) >> 2) * 8 + j) >> 1;
+                    zw[w] = hi;
+                    zw[w + 8 * G::ZW] = lo;   // row + 16
+                }
+            }
+        }
+    }
+    if (dlive) sa.delta[(int64_t)bh * sa.Tq + di] = dl;
+    __syncthreads();
+    for (int o = 0; o < sa.nops; ++o) {
+        const SplitOp& op = sa.op[o];
+        if (tile >= op.ntiles) continue;
+        const int64_t t = (int64_t)bh * op.ntiles + tile;
+        if (op.ext) {
+            u4* g = reinterpret_cast<u4*>(op.ext + t * G::XT);
+            for (int e = tid; e < G::XT / 8; e += 256) g[e] = reinterpret_cast<const u4*>(img + o * IMG)[e];
+        }
+        if (op.z) {
+            u4* g = reinterpret_cast<u4*>(op.z + t * G::ZT);
+            for (int e = tid; e < G::ZT / 8; e += 256) g[e] = reinterpret_cast<const u4*>(img + o * IMG + G::XT)[e];
+        }
+    }
+}
+
+// copy one tile image (global rows of W bf16) into LDS (rows of W + 8 bf16), in two halves so
+// the next tile's loads are in flight during the current tile's MFMAs
+template <int ROWS, int W>
+struct TileCopy {
+    static constexpr int CPR = W / 8;           // 16-byte chunks per row
+    static constexpr int N = ROWS * CPR;
+    static constexpr int IT = (N + 255) / 256;
+    u4 r[IT];
+    __device__ __forceinline__ void load(const uint16_t* g, int tid) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int e = tid + 256 * it;
+            if (N % 256 == 0 || e < N) r[it] = *reinterpret_cast<const u4*>(g + e * 8);
+        }
+    }
+    __device__ __forceinline__ void store(uint16_t* l, int tid) const {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int e = tid + 256 * it;
+            if (N % 256 == 0 || e < N) {
+                const int row = e / CPR, c = e - row * CPR;
+                *reinterpret_cast<u4*>(l + row * (W + 8) + c * 8) = r[it];
+            }
+        }
+    }
+};
+
+
+// register-side ext vector [hi | lo | hi | 0] of this lane's row (v = the row, HDP floats)
+template <int HDP>
+__device__ __forceinline__ void build_y(const float (&v)[HDP], int lg, u4 (&y)[Geo<HDP>::NX]) {
+#pragma unroll
+    for (int c = 0; c < Geo<HDP>::NX; ++c)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int e = 32 * c + 8 * lg + 2 * jj;
+            const int seg = e / HDP, d = e - seg * HDP;
+            float x0 = 0.f, x1 = 0.f;
+#pragma unroll
+            for (int t = 0; t < HDP; ++t) {
+                x0 = t == d ? v[t] : x0;
+                x1 = t == d + 1 ? v[t] : x1;
+            }
+            y[c][jj] = (seg == 0 || seg == 2) ? pk_hi(x0, x1) : (seg == 1 ? pk_lo(x0, x1) : 0u);
+        }
+}
+
+// S-type: acc += X[16 st + (lane & 15)][:] . Y[:]  over the 3-term ext dimension
+template <int HDP>
+__device__ __forceinline__ mf4 sprod(const uint16_t* xe, int st, const u4 (&y)[Geo<HDP>::NX], mf4 acc, int ln,
+                                     int lg) {
+    using G = Geo<HDP>;
+#pragma unroll
+    for (int c = 0; c < G::NX; ++c)
+        acc = mfma_bf(*reinterpret_cast<const u4*>(xe + (16 * st + ln) * G::XS + 32 * c + 8 * lg), y[c], acc);
+    return acc;
+}
+
+// Z-type: acc(d x cols) += Z^T(d x 64 rows) . W(64 rows x cols), W in accumulator layout
+template <int HDP>
+__device__ __forceinline__ mf4 zprod(const uint16_t* z, const mf4 (&w)[4], mf4 acc, int ln, int lg) {
+    using G = Geo<HDP>;
+    if constexpr (G::RS) {
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const u4 A = *reinterpret_cast<const u4*>(z + ln * G::ZS + st * 32 + lg * 8);
+            const u4 B = {pk_hi(w[st][0], w[st][1]), pk_hi(w[st][2], w[st][3]), pk_lo(w[st][0], w[st][1]),
+                          pk_lo(w[st][2], w[st][3])};
+            acc = mfma_bf(A, B, acc);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const mf4 &wa = w[2 * c], &wb = w[2 * c + 1];
+            const u4 Bh = {pk_hi(wa[0], wa[1]), pk_hi(wa[2], wa[3]), pk_hi(wb[0], wb[1]), pk_hi(wb[2], wb[3])};
+            const u4 Bl = {pk_lo(wa[0], wa[1]), pk_lo(wa[2], wa[3]), pk_lo(wb[0], wb[1]), pk_lo(wb[2], wb[3])};
+            const u4 Ah = *reinterpret_cast<const u4*>(z + ln * G::ZS + c * 32 + lg * 8);
+            const u4 Al = *reinterpret_cast<const u4*>(z + (16 + ln) * G::ZS + c * 32 + lg * 8);
+            acc = mfma_bf(Ah, Bh, acc);
+            acc = mfma_bf(Ah, Bl, acc);
+            acc = mfma_bf(Al, Bh, acc);
+        }
+    }
+    return acc;
+}
+
+// the Z-type result: row-split halves summed (rows d = 4 (lg & 1) + i then), else rows d = 4 lg + i
+template <int HDP>
+__device__ __forceinline__ mf4 zfinish(mf4 acc) {
+    if constexpr (Geo<HDP>::RS) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += __shfl_xor(acc[i], 32);
+    }
+    return acc;
+}
+template <int HDP>
+__device__ __forceinline__ bool zrow_owner(int lg) { return Geo<HDP>::RS ? lg < 2 : true; }
+
+// S^T tile of a query-row wave (lane: keys k0 + 16 st + 4 lg + i, query qi): -inf past Tk and
+// under the causal mask (selects, no branches)
+__device__ __forceinline__ void mask_keys(mf4 (&s)[4], int k0, int qi, int lg, const MhaArgs& a) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = k0 + 16 * st + 4 * lg + i;
+            const bool mk = (j >= a.Tk) | ((a.causal > 0) & (j - qi >= a.causal));
+            s[st][i] = mk ? -INFINITY : s[st][i];
+        }
+}
+
+// LDS stages: NBUF = 2 (one barrier per tile, the next tile copied in while this one computes)
+// when a stage fits 20 KB, else 1 (two barriers per tile; keeps >= 4 blocks per CU)
+template <int BYTES>
+struct Stages {
+    static constexpr int N = BYTES <= 20 * 1024 ? 2 : 1;
+};
+
+// the tile loop shared by the three kernels: load(t) fills registers from the images of tile t,
+// store(buf) writes them to LDS stage buf, body(t, buf) computes on stage buf
+template <int NBUF, typename Load, typename Store, typename Body>
+__device__ __forceinline__ void tile_loop(int tb, int te, Load&& load, Store&& store, Body&& body) {
+    if (tb >= te) return;
+    load(tb);
+    if (NBUF == 2) {
+        store(0);
+        if (tb + 1 < te) load(tb + 1);
+        __syncthreads();
+    }
+    for (int t = tb; t < te; ++t) {
+        const int buf = NBUF == 2 ? (t - tb) & 1 : 0;
+        if (NBUF == 1) {
+            if (t > tb) __syncthreads();
+            store(0);
+            __syncthreads();
+            if (t + 1 < te) load(t + 1);
+        }
+        body(t, buf);
+        if (NBUF == 2) {
+            if (t + 1 < te) {
+                store(buf ^ 1);
+                if (t + 2 < te) load(t + 2);
+            }
+            __syncthreads();
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -94,180 +422,197 @@ __device__ __forceinline__ float load_pad(const float* base, int64_t rowoff, int
 // ------------------------------------------------------------------------------------
 template <int HDP, bool DROP>
 __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
-    constexpr int KST = HDP + 1;   // K tile row stride (read as [lane&15][4dc + lane>>4])
-    __shared__ float ks_[MT * KST + 16];
-    __shared__ float vs_[MT * VST + 16];
+    using G = Geo<HDP>;
+    constexpr int SK = MT * G::XS, SV = G::ZR * G::ZS, STAGE = SK + SV;   // K ext + V Z
+    constexpr int NBUF = Stages<STAGE * 2>::N;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * STAGE];
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int q0 = blockIdx.x * MT + wave * 16;
+    const int bx = a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x;
+    const int q0 = bx * MT + wave * 16;
     const int qi = q0 + ln;
     const bool qok = qi < a.Tq;
-    float qb[HDP / 4];
+    u4 qy[G::NX];
+    {
+        float qv[HDP];
+        const int64_t rq = ((int64_t)qi * a.B + b) * a.qs + h * a.hd;
 #pragma unroll
-    for (int dc = 0; dc < HDP / 4; ++dc)
-        qb[dc] = load_pad(a.q, ((int64_t)qi * a.B + b) * a.qs + h * a.hd, 4 * dc + lg, a.hd, qok) * a.scale2;
+        for (int d = 0; d < HDP; ++d) qv[d] = load_pad(a.q, rq, d, a.hd, qok) * a.scale2;
+        build_y<HDP>(qv, lg, qy);
+    }
+    const bool ones = !DROP && a.hd < HDP;   // the denominator as V's padding row of ones (host sets it)
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
+    const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
+    const uint16_t* vzg = a.vz + (int64_t)bh * a.nkt * G::ZT;
+    TileCopy<MT, G::EW> ck;
+    TileCopy<G::ZR, G::ZW> cv;
     mf4 o = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
-    const int kend_blk = key_end(a, min(a.Tq - 1, (int)blockIdx.x * MT + MT - 1));
+    const int kend_blk = key_end(a, min(a.Tq - 1, bx * MT + MT - 1));
     const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 15)) : 0;
-    for (int k0 = 0; k0 < kend_blk; k0 += MT) {
-        __syncthreads();
-        for (int e = tid; e < MT * HDP; e += 256) {
-            const int r = e / HDP, c = e - r * HDP, j = k0 + r;
-            const bool ok = j < a.Tk;
-            ks_[r * KST + c] = load_pad(a.k, ((int64_t)j * a.B + b) * a.ks + h * a.hd, c, a.hd, ok);
-            vs_[r * VST + c] = load_pad(a.v, ((int64_t)j * a.B + b) * a.vs + h * a.hd, c, a.hd, ok);
-        }
-        __syncthreads();
-        if (k0 >= kend_w) continue;   // wave-uniform: every key of the tile is masked for this wave
-        mf4 s[4];
+    tile_loop<NBUF>(
+        0, (kend_blk + MT - 1) / MT,
+        [&](int t) {
+            ck.load(kxg + (int64_t)t * G::XT, tid);
+            cv.load(vzg + (int64_t)t * G::ZT, tid);
+        },
+        [&](int buf) {
+            ck.store(lds + buf * STAGE, tid);
+            cv.store(lds + buf * STAGE + SK, tid);
+        },
+        [&](int t, int buf) {
+            const int k0 = t * MT;
+            if (k0 >= kend_w) return;   // wave-uniform: every key of the tile is masked for this wave
+            const uint16_t* kx = lds + buf * STAGE;
+            const uint16_t* vz = kx + SK;
+            mf4 s[4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            s[st] = (mf4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int dc = 0; dc < HDP / 4; ++dc) s[st] = mfma4(ks_[(16 * st + ln) * KST + 4 * dc + lg], qb[dc], s[st]);
-        }
-        // lane: s[st][i] = S^T[key k0 + 16 st + 4 lg + i][query qi] (log2 domain)
-        const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
-        if (edge) {
+            for (int st = 0; st < 4; ++st) s[st] = sprod<HDP>(kx, st, qy, (mf4){0.f, 0.f, 0.f, 0.f}, ln, lg);
+            // lane: s[st][i] = S^T[key k0 + 16 st + 4 lg + i][query qi] (log2 domain)
+            const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
+            if (edge) mask_keys(s, k0, qi, lg, a);
+            float mx = -INFINITY;
 #pragma unroll
             for (int st = 0; st < 4; ++st)
 #pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[st][i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mn = fmaxf(m, mx);
+            const float ms = mn == -INFINITY ? 0.f : mn;   // no visible key yet: every p below is 0
+            const float alpha = fast_exp2(m - ms);
+            m = mn;
+            o *= alpha;
+            if (!ones) lsum *= alpha;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+#pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int j = k0 + 16 * st + 4 * lg + i;
-                    if (j >= a.Tk || (a.causal > 0 && j - qi >= a.causal)) s[st][i] = -INFINITY;
+                    const float p = fast_exp2(s[st][i] - ms);
+                    float pv = p;
+                    if (!ones) lsum += p;
+                    if (DROP) pv = drop_keep(rowh, k0 + 16 * st + 4 * lg + i, a.thresh) ? p * a.inv_keep : 0.f;
+                    s[st][i] = pv;
                 }
-        }
-        float mx = -INFINITY;
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[st][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mn = fmaxf(m, mx);
-        const float ms = mn == -INFINITY ? 0.f : mn;   // no visible key yet: every p below is 0
-        const float alpha = fast_exp2(m - ms);
-        m = mn;
-        lsum *= alpha;
-        o *= alpha;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float p = fast_exp2(s[st][i] - ms);
-                lsum += p;
-                float pv = p;
-                if (DROP) pv = drop_keep(rowh, k0 + 16 * st + 4 * lg + i, a.thresh) ? p * a.inv_keep : 0.f;
-                s[st][i] = pv;
             }
-        }
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o = mfma4(vs_[(16 * st + 4 * lg + i) * VST + ln], s[st][i], o);
+            o = zprod<HDP>(vz, s, o, ln, lg);
+        });
+    o = zfinish<HDP>(o);
+    if (ones) {
+        const int hd = a.hd, src = ((hd >> 2) << 4) + ln, i = hd & 3;
+        const float t = i == 0 ? o[0] : (i == 1 ? o[1] : (i == 2 ? o[2] : o[3]));
+        lsum = __shfl(t, src);
+    } else {
+        lsum += __shfl_xor(lsum, 16);
+        lsum += __shfl_xor(lsum, 32);
     }
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
     if (qok) {
         const float inv = 1.0f / lsum;
         float* orow = a.out + ((int64_t)qi * a.B + b) * a.os + h * a.hd;
+        if (zrow_owner<HDP>(lg)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int d = 4 * lg + i;
-            if (d < a.hd) orow[d] = o[i] * inv;
+            for (int i = 0; i < 4; ++i) {
+                const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
+                if (d < a.hd) orow[d] = o[i] * inv;
+            }
         }
         if (lg == 0) a.lse[(int64_t)bh * a.Tq + qi] = (m + fast_log2(lsum)) * kLn2;
     }
 }
 
-// delta = rowsum(dO * O) per (b, h, i): with dropout O is the dropped output, which is exactly
-// the p-weighted mean of the dropped-probability gradient the backward needs
-__global__ __launch_bounds__(256) void mha_delta_kernel(MhaArgs a) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (i, b, h)
-    if (e >= (int64_t)a.Tq * a.B * a.H) return;
-    const int h = (int)(e % a.H);
-    const int64_t ib = e / a.H;
-    const int b = (int)(ib % a.B), i = (int)(ib / a.B);
-    const float* o = a.o + ib * a.os + h * a.hd;
-    const float* g = a.dout + ib * a.os + h * a.hd;
-    float d = 0.f;
-    for (int c = 0; c < a.hd; ++c) d = fmaf(o[c], g[c], d);
-    a.delta[((int64_t)b * a.H + h) * a.Tq + i] = d;
-}
-
 // ------------------------------------------------------------------------------------
 // dq: wave = 16 queries, loops over key tiles
 // ------------------------------------------------------------------------------------
+template <int HDP>
+struct DqLds {
+    using G = Geo<HDP>;
+    static constexpr int SX = MT * G::XS, SZ = G::ZR * G::ZS, STAGE = 2 * SX + SZ;   // K ext, V ext, K Z
+    static constexpr int NBUF = Stages<STAGE * 2>::N;
+    static constexpr int BYTES = NBUF * STAGE * 2;
+};
 template <int HDP, bool DROP>
-__global__ __launch_bounds__(256) void mha_dq_mfma_kernel(MhaArgs a) {
-    constexpr int KST = HDP + 1;
-    __shared__ float ks_[MT * KST + 16];   // read as A[key][d] (S^T) and as A[d = lane&15][key] (dQ^T)
-    __shared__ float vs_[MT * KST + 16];   // read as A[key][d] (dP^T)
+__device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int bx) {
+    using G = Geo<HDP>;
+    constexpr int SX = DqLds<HDP>::SX, SZ = DqLds<HDP>::SZ, STAGE = DqLds<HDP>::STAGE;
+    constexpr int NBUF = DqLds<HDP>::NBUF;
+    (void)SZ;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int q0 = blockIdx.x * MT + wave * 16;
+    const int q0 = bx * MT + wave * 16;
     const int qi = q0 + ln;
     const bool qok = qi < a.Tq;
-    float qb[HDP / 4], gb[HDP / 4];
     const int64_t rq = ((int64_t)qi * a.B + b) * a.qs + h * a.hd, ro = ((int64_t)qi * a.B + b) * a.os + h * a.hd;
+    u4 qy[G::NX], gy[G::NX];
+    {
+        float qv[HDP], gv[HDP];
 #pragma unroll
-    for (int dc = 0; dc < HDP / 4; ++dc) {
-        qb[dc] = load_pad(a.q, rq, 4 * dc + lg, a.hd, qok) * a.scale2;
-        gb[dc] = load_pad(a.dout, ro, 4 * dc + lg, a.hd, qok);
+        for (int d = 0; d < HDP; ++d) {
+            qv[d] = load_pad(a.q, rq, d, a.hd, qok) * a.scale2;
+            gv[d] = load_pad(a.dout, ro, d, a.hd, qok);
+        }
+        build_y<HDP>(qv, lg, qy);
+        build_y<HDP>(gv, lg, gy);
     }
     const float lse2 = qok ? a.lse[(int64_t)bh * a.Tq + qi] * kLog2e : INFINITY;
     const float dl = qok ? a.delta[(int64_t)bh * a.Tq + qi] : 0.f;
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
+    const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
+    const uint16_t* vxg = a.vx + (int64_t)bh * a.nkt * G::XT;
+    const uint16_t* kzg = a.kz + (int64_t)bh * a.nkt * G::ZT;
+    TileCopy<MT, G::EW> ck, cv;
+    TileCopy<G::ZR, G::ZW> cz;
+    const mf4 sinit = {-lse2, -lse2, -lse2, -lse2};
+    const float di = DROP ? 0.f : -dl;
+    const mf4 dinit = {di, di, di, di};
     mf4 dq = {0.f, 0.f, 0.f, 0.f};
-    const int kend_blk = key_end(a, min(a.Tq - 1, (int)blockIdx.x * MT + MT - 1));
+    const int kend_blk = key_end(a, min(a.Tq - 1, bx * MT + MT - 1));
     const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 15)) : 0;
-    for (int k0 = 0; k0 < kend_blk; k0 += MT) {
-        __syncthreads();
-        for (int e = tid; e < MT * HDP; e += 256) {
-            const int r = e / HDP, c = e - r * HDP, j = k0 + r;
-            const bool ok = j < a.Tk;
-            ks_[r * KST + c] = load_pad(a.k, ((int64_t)j * a.B + b) * a.ks + h * a.hd, c, a.hd, ok);
-            vs_[r * KST + c] = load_pad(a.v, ((int64_t)j * a.B + b) * a.vs + h * a.hd, c, a.hd, ok);
-        }
-        __syncthreads();
-        if (k0 >= kend_w) continue;
-        mf4 s[4], dp[4];
+    tile_loop<NBUF>(
+        0, (kend_blk + MT - 1) / MT,
+        [&](int t) {
+            ck.load(kxg + (int64_t)t * G::XT, tid);
+            cv.load(vxg + (int64_t)t * G::XT, tid);
+            cz.load(kzg + (int64_t)t * G::ZT, tid);
+        },
+        [&](int buf) {
+            uint16_t* st = lds + buf * STAGE;
+            ck.store(st, tid);
+            cv.store(st + SX, tid);
+            cz.store(st + 2 * SX, tid);
+        },
+        [&](int t, int buf) {
+            const int k0 = t * MT;
+            if (k0 >= kend_w) return;
+            const uint16_t* kx = lds + buf * STAGE;
+            const uint16_t* vx = kx + SX;
+            const uint16_t* kz = kx + 2 * SX;
+            mf4 s[4], dp[4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            s[st] = (mf4){0.f, 0.f, 0.f, 0.f};
-            dp[st] = (mf4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int dc = 0; dc < HDP / 4; ++dc) {
-                s[st] = mfma4(ks_[(16 * st + ln) * KST + 4 * dc + lg], qb[dc], s[st]);
-                dp[st] = mfma4(vs_[(16 * st + ln) * KST + 4 * dc + lg], gb[dc], dp[st]);
+            for (int st = 0; st < 4; ++st) {
+                s[st] = sprod<HDP>(kx, st, qy, sinit, ln, lg);    // S^T - lse2
+                dp[st] = sprod<HDP>(vx, st, gy, dinit, ln, lg);   // dP^T (- delta)
             }
-        }
-        const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
+            const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
+            if (edge) mask_keys(s, k0, qi, lg, a);
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
+            for (int st = 0; st < 4; ++st) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = k0 + 16 * st + 4 * lg + i;
-                float p = fast_exp2(s[st][i] - lse2);
-                if (edge && (j >= a.Tk || (a.causal > 0 && j - qi >= a.causal))) p = 0.f;
-                float g = dp[st][i];
-                if (DROP) g = drop_keep(rowh, j, a.thresh) ? g * a.inv_keep : 0.f;
-                s[st][i] = p * (g - dl);   // dS^T
+                for (int i = 0; i < 4; ++i) {
+                    const int j = k0 + 16 * st + 4 * lg + i;
+                    const float p = fast_exp2(s[st][i]);
+                    float g = dp[st][i];
+                    if (DROP) g = (drop_keep(rowh, j, a.thresh) ? g * a.inv_keep : 0.f) - dl;
+                    s[st][i] = p * g;   // dS^T
+                }
             }
-        }
-        // dQ^T(d x queries) += K^T dS^T: A[m = d][k = key] = K[16 st + 4 lg + i][lane & 15]
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dq = mfma4(ks_[(16 * st + 4 * lg + i) * KST + ln], s[st][i], dq);
-    }
-    if (qok) {
+            dq = zprod<HDP>(kz, s, dq, ln, lg);   // dQ^T += K^T dS^T
+        });
+    dq = zfinish<HDP>(dq);
+    if (qok && zrow_owner<HDP>(lg)) {
         float* drow = a.dq + rq;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int d = 4 * lg + i;
+            const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
             if (d < a.hd) drow[d] = dq[i] * a.scale;
         }
     }
@@ -276,98 +621,155 @@ __global__ __launch_bounds__(256) void mha_dq_mfma_kernel(MhaArgs a) {
 // ------------------------------------------------------------------------------------
 // dk, dv: wave = 16 keys, loops over query tiles
 // ------------------------------------------------------------------------------------
+template <int HDP>
+struct DkvLds {
+    using G = Geo<HDP>;
+    static constexpr int SX = MT * G::XS, SZ = G::ZR * G::ZS;
+    static constexpr int STAGE = 2 * SX + 2 * SZ + 4 * MT;   // Q ext, dO ext, Q Z, dO Z, -lse2 and -delta (fp32)
+    static constexpr int NBUF = Stages<STAGE * 2>::N;
+    static constexpr int BYTES = NBUF * STAGE * 2;
+};
 template <int HDP, bool DROP>
-__global__ __launch_bounds__(256) void mha_dkv_mfma_kernel(MhaArgs a) {
-    constexpr int QST = 17;                // read as A[query][d] and as A[d = lane&15][query 4g+i]
-    __shared__ float qs_[MT * QST + 16];   // q * scale * log2e
-    __shared__ float gs_[MT * QST + 16];   // dO
-    __shared__ float ls_[MT];              // lse2
-    __shared__ float ds_[MT];              // delta
+__device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, int bx) {
+    using G = Geo<HDP>;
+    constexpr int SX = DkvLds<HDP>::SX, SZ = DkvLds<HDP>::SZ, STAGE = DkvLds<HDP>::STAGE;
+    constexpr int NBUF = DkvLds<HDP>::NBUF;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int j0 = blockIdx.x * MT + wave * 16;
+    const int j0 = bx * MT + wave * 16;
     const int kj = j0 + ln;
     const bool kok = kj < a.Tk;
-    float kb[HDP / 4], vb[HDP / 4];
     const int64_t rk = ((int64_t)kj * a.B + b) * a.ks + h * a.hd, rv = ((int64_t)kj * a.B + b) * a.vs + h * a.hd;
+    u4 ky[G::NX], vy[G::NX];
+    {
+        float kv[HDP], vv[HDP];
 #pragma unroll
-    for (int dc = 0; dc < HDP / 4; ++dc) {
-        kb[dc] = load_pad(a.k, rk, 4 * dc + lg, a.hd, kok);
-        vb[dc] = load_pad(a.v, rv, 4 * dc + lg, a.hd, kok);
+        for (int d = 0; d < HDP; ++d) {
+            kv[d] = load_pad(a.k, rk, d, a.hd, kok);
+            vv[d] = load_pad(a.v, rv, d, a.hd, kok);
+        }
+        build_y<HDP>(kv, lg, ky);
+        build_y<HDP>(vv, lg, vy);
     }
+    const uint16_t* qxg = a.qx + (int64_t)bh * a.nqt * G::XT;
+    const uint16_t* gxg = a.gx + (int64_t)bh * a.nqt * G::XT;
+    const uint16_t* qzg = a.qz + (int64_t)bh * a.nqt * G::ZT;
+    const uint16_t* gzg = a.gz + (int64_t)bh * a.nqt * G::ZT;
+    TileCopy<MT, G::EW> cq, cg;
+    TileCopy<G::ZR, G::ZW> czq, czg;
+    float pl = 0.f, pd_ = 0.f;   // the tile's -lse2 / -delta (threads < MT)
     mf4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
     // first query that can see the block's first key: j - i < diag  <=>  i > j - diag
     int i_begin = 0;
-    if (a.causal > 0) i_begin = max(0, (int)blockIdx.x * MT - a.causal + 1);
-    i_begin = i_begin / MT * MT;
+    if (a.causal > 0) i_begin = max(0, bx * MT - a.causal + 1);
     const int ib_w = a.causal > 0 ? max(0, j0 - a.causal + 1) : 0;   // this wave's first visible query
-    for (int i0 = i_begin; i0 < a.Tq; i0 += MT) {
-        __syncthreads();
-        for (int e = tid; e < MT * HDP; e += 256) {
-            const int r = e / HDP, c = e - r * HDP, i = i0 + r;
-            const bool ok = i < a.Tq;
-            qs_[r * QST + c] = load_pad(a.q, ((int64_t)i * a.B + b) * a.qs + h * a.hd, c, a.hd, ok) * a.scale2;
-            gs_[r * QST + c] = load_pad(a.dout, ((int64_t)i * a.B + b) * a.os + h * a.hd, c, a.hd, ok);
-        }
-        for (int e = tid; e < MT; e += 256) {
-            const int i = i0 + e;
-            ls_[e] = i < a.Tq ? a.lse[(int64_t)bh * a.Tq + i] * kLog2e : INFINITY;
-            ds_[e] = i < a.Tq ? a.delta[(int64_t)bh * a.Tq + i] : 0.f;
-        }
-        __syncthreads();
-        if (i0 + MT <= ib_w || j0 >= a.Tk) continue;   // wave-uniform: nothing visible
-        mf4 s[4], dp[4];
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            s[st] = (mf4){0.f, 0.f, 0.f, 0.f};
-            dp[st] = (mf4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int dc = 0; dc < HDP / 4; ++dc) {
-                s[st] = mfma4(qs_[(16 * st + ln) * QST + 4 * dc + lg], kb[dc], s[st]);
-                dp[st] = mfma4(gs_[(16 * st + ln) * QST + 4 * dc + lg], vb[dc], dp[st]);
+    tile_loop<NBUF>(
+        i_begin / MT, a.nqt,
+        [&](int t) {
+            cq.load(qxg + (int64_t)t * G::XT, tid);
+            cg.load(gxg + (int64_t)t * G::XT, tid);
+            czq.load(qzg + (int64_t)t * G::ZT, tid);
+            czg.load(gzg + (int64_t)t * G::ZT, tid);
+            if (tid < MT) {
+                const int i = t * MT + tid;
+                pl = i < a.Tq ? -a.lse[(int64_t)bh * a.Tq + i] * kLog2e : -INFINITY;
+                pd_ = i < a.Tq ? -a.delta[(int64_t)bh * a.Tq + i] : 0.f;
             }
-        }
-        // lane: s[st][i] = S[query i0 + 16 st + 4 lg + i][key kj]
-        const bool edge = (i0 + MT > a.Tq) || !kok || (a.causal > 0 && i0 < j0 + 16 - a.causal + 1);
-        mf4 pd[4];
+        },
+        [&](int buf) {
+            uint16_t* st = lds + buf * STAGE;
+            cq.store(st, tid);
+            cg.store(st + SX, tid);
+            czq.store(st + 2 * SX, tid);
+            czg.store(st + 2 * SX + SZ, tid);
+            float* f = reinterpret_cast<float*>(st + 2 * SX + 2 * SZ);
+            if (tid < MT) {
+                f[tid] = pl;
+                f[MT + tid] = pd_;
+            }
+        },
+        [&](int t, int buf) {
+            const int i0 = t * MT;
+            if (i0 + MT <= ib_w || j0 >= a.Tk) return;   // wave-uniform: nothing visible
+            const uint16_t* qx = lds + buf * STAGE;
+            const uint16_t* gx = qx + SX;
+            const uint16_t* qz = qx + 2 * SX;
+            const uint16_t* gz = qz + SZ;
+            const float* ls_ = reinterpret_cast<const float*>(qx + 2 * SX + 2 * SZ);
+            const float* ds_ = ls_ + MT;
+            mf4 s[4], dp[4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = 16 * st + 4 * lg + i, qi = i0 + r;
-                float p = fast_exp2(s[st][i] - ls_[r]);
-                if (edge && (qi >= a.Tq || !kok || (a.causal > 0 && kj - qi >= a.causal))) p = 0.f;
-                float g = dp[st][i], pv = p;
-                if (DROP) {
-                    const bool kp = drop_keep(drop_row(a.seed, bh, a.Tq, qi), kj, a.thresh);
-                    g = kp ? g * a.inv_keep : 0.f;
-                    pv = kp ? p * a.inv_keep : 0.f;
+            for (int st = 0; st < 4; ++st) {
+                const float2 l01 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg);
+                const float2 l23 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg + 2);
+                s[st] = sprod<HDP>(qx, st, ky, (mf4){l01.x, l01.y, l23.x, l23.y}, ln, lg);   // S - lse2
+                mf4 di = {0.f, 0.f, 0.f, 0.f};
+                if (!DROP) {
+                    const float2 d01 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg);
+                    const float2 d23 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg + 2);
+                    di = (mf4){d01.x, d01.y, d23.x, d23.y};
                 }
-                pd[st][i] = pv;
-                s[st][i] = p * (g - ds_[r]);   // dS
+                dp[st] = sprod<HDP>(gx, st, vy, di, ln, lg);   // dP (- delta)
             }
-        }
-        // dV^T(d x keys) += dO^T Pd, dK^T += Q2^T dS: A[m = d][k = query] = X[16 st + 4 lg + i][lane & 15]
+            // lane: s[st][i] = S[query i0 + 16 st + 4 lg + i][key kj]
+            const bool edge = (i0 + MT > a.Tq) || !kok || (a.causal > 0 && i0 < j0 + 16 - a.causal + 1);
+            if (edge) {
 #pragma unroll
-        for (int st = 0; st < 4; ++st)
+                for (int st = 0; st < 4; ++st)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = 16 * st + 4 * lg + i;
-                dv = mfma4(gs_[r * QST + ln], pd[st][i], dv);
-                dk = mfma4(qs_[r * QST + ln], s[st][i], dk);
+                    for (int i = 0; i < 4; ++i) {
+                        const int qi = i0 + 16 * st + 4 * lg + i;
+                        const bool mk = (qi >= a.Tq) | !kok | ((a.causal > 0) & (kj - qi >= a.causal));
+                        s[st][i] = mk ? -INFINITY : s[st][i];
+                    }
             }
-    }
-    if (kok) {
+            mf4 pd[4];
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 16 * st + 4 * lg + i, qi = i0 + r;
+                    const float p = fast_exp2(s[st][i]);
+                    float g = dp[st][i], pv = p;
+                    if (DROP) {
+                        const bool kp = drop_keep(drop_row(a.seed, bh, a.Tq, qi), kj, a.thresh);
+                        g = (kp ? g * a.inv_keep : 0.f) + ds_[r];
+                        pv = kp ? p * a.inv_keep : 0.f;
+                    }
+                    pd[st][i] = pv;
+                    s[st][i] = p * g;   // dS
+                }
+            }
+            dv = zprod<HDP>(gz, pd, dv, ln, lg);   // dV^T += dO^T Pd
+            dk = zprod<HDP>(qz, s, dk, ln, lg);    // dK^T += Q2^T dS
+        });
+    dk = zfinish<HDP>(dk);
+    dv = zfinish<HDP>(dv);
+    if (kok && zrow_owner<HDP>(lg)) {
         float* krow = a.dk + rk;
         float* vrow = a.dv + rv;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int d = 4 * lg + i;
+            const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
             if (d < a.hd) {
                 krow[d] = dk[i] * kLn2;   // staged q2 = q * scale * log2e
                 vrow[d] = dv[i];
             }
         }
+    }
+}
+
+// the backward's two halves in one launch: z = 0 dq blocks (query tiles), z = 1 dk/dv blocks (key
+// tiles); dq's causal tail overlaps the first dk/dv blocks
+template <int HDP, bool DROP>
+__global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(MhaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lds[];
+    if (blockIdx.z == 0) {
+        if ((int)blockIdx.x >= a.nqt) return;
+        mha_dq_body<HDP, DROP>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x);
+    } else {
+        if ((int)blockIdx.x >= a.nkt) return;
+        mha_dkv_body<HDP, DROP>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nkt) : (int)blockIdx.x);
     }
 }
 
@@ -427,41 +829,99 @@ static int mha_fill(const mmni_mha_desc* d, MhaArgs& a) {
     const double t = keep * 4294967296.0;
     a.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
     a.seed = d->seed;
+    a.nqt = (a.Tq + MT - 1) / MT;
+    a.nkt = (a.Tk + MT - 1) / MT;
     return 0;
 }
 
 static int hd_pad(int hd) { return hd <= 4 ? 4 : (hd <= 8 ? 8 : 16); }
 
+// workspace: 256-byte aligned segments.  forward: K ext + V Z images; backward: delta, then
+// K ext, K Z, V ext (key tiles) and Q ext, Q Z, dO ext, dO Z (query tiles)
+struct MhaWs {
+    size_t delta, kx, kz, vx, vz, qx, qz, gx, gz, total;
+};
+static MhaWs mha_ws_layout(const MhaArgs& a, bool bwd) {
+    const int HDP = hd_pad(a.hd);
+    const int NX = (3 * HDP + 31) / 32, EW = 32 * NX, ZR = HDP <= 8 ? 16 : 32, ZW = HDP <= 8 ? 128 : 64;
+    const size_t bhn = (size_t)a.B * a.H, xt = (size_t)MT * EW * 2, zt = (size_t)ZR * ZW * 2;
+    const size_t nk = bhn * ((a.Tk + MT - 1) / MT), nq = bhn * ((a.Tq + MT - 1) / MT);
+    MhaWs w{};
+    size_t off = 0;
+    auto seg = [&](size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    if (!bwd) {
+        w.kx = seg(nk * xt);
+        w.vz = seg(nk * zt);
+    } else {
+        w.delta = seg(bhn * a.Tq * sizeof(float));
+        w.kx = seg(nk * xt);
+        w.kz = seg(nk * zt);
+        w.vx = seg(nk * xt);
+        w.qx = seg(nq * xt);
+        w.qz = seg(nq * zt);
+        w.gx = seg(nq * xt);
+        w.gz = seg(nq * zt);
+    }
+    w.total = off;
+    return w;
+}
+
 template <int HDP, bool DROP>
-static int mha_fwd_launch(MhaArgs& a, hipStream_t s) {
-    dim3 grid((a.Tq + MT - 1) / MT, a.B * a.H);
+static int mha_fwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
+    const MhaWs w = mha_ws_layout(a, false);
+    uint16_t* kx = reinterpret_cast<uint16_t*>(ws + w.kx);
+    uint16_t* vz = reinterpret_cast<uint16_t*>(ws + w.vz);
+    SplitArgs sa{};
+    sa.B = a.B; sa.H = a.H; sa.hd = a.hd;
+    sa.op[0] = SplitOp{a.k, a.ks, a.Tk, a.nkt, 1.f, -1, kx, nullptr};
+    sa.op[1] = SplitOp{a.v, a.vs, a.Tk, a.nkt, 1.f, (!DROP && a.hd < HDP) ? a.hd : -1, nullptr, vz};
+    sa.nops = 2;
+    mha_split_kernel<HDP><<<dim3(a.nkt, a.B * a.H), 256, 0, s>>>(sa);
+    int rc = launch_status("mha_split");
+    if (rc) return rc;
+    a.kx = kx;
+    a.vz = vz;
+    dim3 grid(a.nqt, a.B * a.H);
     mha_fwd_mfma_kernel<HDP, DROP><<<grid, 256, 0, s>>>(a);
     return launch_status("mha_fwd");
 }
 
 template <int HDP, bool DROP>
-static int mha_bwd_launch(MhaArgs& a, hipStream_t s) {
-    const int64_t n = (int64_t)a.Tq * a.B * a.H;
-    mha_delta_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
-    int rc = launch_status("mha_delta");
+static int mha_bwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
+    const MhaWs w = mha_ws_layout(a, true);
+    a.delta = reinterpret_cast<float*>(ws + w.delta);
+    auto img = [&](size_t off) { return reinterpret_cast<uint16_t*>(ws + off); };
+    SplitArgs sa{};
+    sa.B = a.B; sa.H = a.H; sa.hd = a.hd;
+    sa.op[0] = SplitOp{a.k, a.ks, a.Tk, a.nkt, 1.f, -1, img(w.kx), img(w.kz)};
+    sa.op[1] = SplitOp{a.v, a.vs, a.Tk, a.nkt, 1.f, -1, img(w.vx), nullptr};
+    sa.op[2] = SplitOp{a.q, a.qs, a.Tq, a.nqt, a.scale2, -1, img(w.qx), img(w.qz)};
+    sa.op[3] = SplitOp{a.dout, a.os, a.Tq, a.nqt, 1.f, -1, img(w.gx), img(w.gz)};
+    sa.nops = 4;
+    sa.o = a.o; sa.g = a.dout; sa.os = a.os; sa.Tq = a.Tq; sa.delta = a.delta;
+    mha_split_kernel<HDP><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H), 256, 0, s>>>(sa);
+    int rc = launch_status("mha_split");
     if (rc) return rc;
-    dim3 gq((a.Tq + MT - 1) / MT, a.B * a.H);
-    mha_dq_mfma_kernel<HDP, DROP><<<gq, 256, 0, s>>>(a);
-    rc = launch_status("mha_bwd_dq");
-    if (rc) return rc;
-    dim3 gk((a.Tk + MT - 1) / MT, a.B * a.H);
-    mha_dkv_mfma_kernel<HDP, DROP><<<gk, 256, 0, s>>>(a);
-    return launch_status("mha_bwd_dkv");
+    a.kx = img(w.kx); a.kz = img(w.kz); a.vx = img(w.vx);
+    a.qx = img(w.qx); a.qz = img(w.qz); a.gx = img(w.gx); a.gz = img(w.gz);
+    const int lds = DqLds<HDP>::BYTES > DkvLds<HDP>::BYTES ? DqLds<HDP>::BYTES : DkvLds<HDP>::BYTES;
+    mha_bwd_mfma_kernel<HDP, DROP><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H, 2), 256, lds, s>>>(a);
+    return launch_status("mha_bwd");
 }
 
 #define MMNI_MHA_DISPATCH(FN)                                                             \
     {                                                                                     \
         const bool drop = a.thresh != 0xffffffffu;                                        \
         hipStream_t st_ = (hipStream_t)stream;                                            \
+        char* ws_ = static_cast<char*>(workspace);                                        \
         switch (hd_pad(a.hd)) {                                                           \
-            case 4: return drop ? FN<4, true>(a, st_) : FN<4, false>(a, st_);             \
-            case 8: return drop ? FN<8, true>(a, st_) : FN<8, false>(a, st_);             \
-            default: return drop ? FN<16, true>(a, st_) : FN<16, false>(a, st_);          \
+            case 4: return drop ? FN<4, true>(a, ws_, st_) : FN<4, false>(a, ws_, st_);   \
+            case 8: return drop ? FN<8, true>(a, ws_, st_) : FN<8, false>(a, ws_, st_);   \
+            default: return drop ? FN<16, true>(a, ws_, st_) : FN<16, false>(a, ws_, st_); \
         }                                                                                 \
     }
 
@@ -469,25 +929,39 @@ static int mha_bwd_launch(MhaArgs& a, hipStream_t s) {
 
 using namespace mmni;
 
+extern "C" size_t mmni_mha_fwd_workspace_bytes(const mmni_mha_desc* d) {
+    MhaArgs a{};
+    if (mha_fill(d, a)) return 0;
+    return mha_ws_layout(a, false).total;
+}
+
+extern "C" size_t mmni_mha_bwd_workspace_bytes(const mmni_mha_desc* d) {
+    MhaArgs a{};
+    if (mha_fill(d, a)) return 0;
+    return mha_ws_layout(a, true).total;
+}
+
 extern "C" int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                            float* out, float* lse, void* stream) {
+                            float* out, float* lse, void* workspace, void* stream) {
     MhaArgs a{};
     int rc = mha_fill(d, a);
     if (rc) return rc;
-    MMNI_ARG_CHECK(q && k && v && out && lse, "mha_fwd: null pointer");
+    MMNI_ARG_CHECK(q && k && v && out && lse && workspace, "mha_fwd: null pointer");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(workspace) % 256 == 0, "mha_fwd: workspace must be 256-byte aligned");
     a.q = q; a.k = k; a.v = v; a.out = out; a.lse = lse;
     MMNI_MHA_DISPATCH(mha_fwd_launch)
 }
 
 extern "C" int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
                             const float* out, const float* dout, const float* lse, float* dq, float* dk,
-                            float* dv, float* workspace, void* stream) {
+                            float* dv, void* workspace, void* stream) {
     MhaArgs a{};
     int rc = mha_fill(d, a);
     if (rc) return rc;
     MMNI_ARG_CHECK(q && k && v && out && dout && lse && dq && dk && dv && workspace, "mha_bwd: null pointer");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(workspace) % 256 == 0, "mha_bwd: workspace must be 256-byte aligned");
     a.q = q; a.k = k; a.v = v; a.o = out; a.dout = dout; a.lse = const_cast<float*>(lse);
-    a.dq = dq; a.dk = dk; a.dv = dv; a.delta = workspace;
+    a.dq = dq; a.dk = dk; a.dv = dv;
     MMNI_MHA_DISPATCH(mha_bwd_launch)
 }
 

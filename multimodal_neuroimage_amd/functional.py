@@ -238,6 +238,11 @@ def relative_index(geom, device):
 # ----------------------------------------------------------------------------------------
 # crossmodal multi-head attention core
 # ----------------------------------------------------------------------------------------
+def _workspace(nbytes, device):
+    """Scratch for a kernel call (the caching allocator's blocks are >= 512-byte aligned)."""
+    return torch.empty(max(int(nbytes), 256), device=device, dtype=torch.uint8)
+
+
 def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_, dropout=0.0, seed=0):
     d = _lib.MhaDesc()
     d.Tq, d.Tk, d.B, d.heads, d.head_dim = Tq, Tk, B, heads, hd
@@ -269,9 +274,11 @@ class _MHA(torch.autograd.Function):
         out = torch.empty((Tq, B, E), device=q.device, dtype=torch.float32)
         lse = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
         d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
+        lib = _lib.load()
+        ws = _workspace(lib.mmni_mha_fwd_workspace_bytes(d), q.device)
         ev = KernelTimer.start()
-        check(_lib.load().mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse),
-                                        stream_handle(q.device)), "mmni_mha_fwd")
+        check(lib.mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse), ptr(ws),
+                               stream_handle(q.device)), "mmni_mha_fwd")
         KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.cfg = (heads, causal_diag, scale, dropout, seed)
@@ -288,11 +295,12 @@ class _MHA(torch.autograd.Function):
         dq = torch.empty_like(q)
         dk = torch.empty_like(k)
         dv = torch.empty_like(v)
-        ws = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
         d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
+        lib = _lib.load()
+        ws = _workspace(lib.mmni_mha_bwd_workspace_bytes(d), q.device)
         ev = KernelTimer.start()
-        check(_lib.load().mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
-                                        ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
+        check(lib.mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
+                               ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
               "mmni_mha_bwd")
         KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
         return dq, dk, dv, None, None, None, None, None

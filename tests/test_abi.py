@@ -72,9 +72,9 @@ def test_mha_and_conv_reject_bad_descriptors():
     d.Tq, d.Tk, d.B, d.heads, d.head_dim, d.causal_diag, d.scale = 8, 8, 1, 2, 17, 0, 1.0
     d.q_stride = d.k_stride = d.v_stride = d.o_stride = 34
     p = ctypes.c_void_p(16)
-    assert lib.mmni_mha_fwd(d, p, p, p, p, p, None) == -2
+    assert lib.mmni_mha_fwd(d, p, p, p, p, p, p, None) == -2
     d.head_dim, d.dropout = 8, 1.0
-    assert lib.mmni_mha_fwd(d, p, p, p, p, p, None) < 0
+    assert lib.mmni_mha_fwd(d, p, p, p, p, p, p, None) < 0
     assert "dropout" in lib.mmni_last_error().decode()
     c = _lib.Conv3dDesc()
     for k, v in dict(B=1, D=8, H=8, W=8, Cin=1, Cout=12, kd=4, kh=4, kw=4, sd=4, sh=4, sw=4, pd=0, ph=0, pw=0,
