@@ -181,23 +181,49 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
     constexpr int DP = HDP / 2, NB = 32 * DP;   // 2 x 2 blocks (rows r, r+1; dims d, d+1) per operand
     constexpr int IT = (4 * NB + 255) / 256;
     float x[IT][2][2];
+    bool live[IT];
+    int T_[IT], ones_[IT];
+    float mul_[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         // NB is a multiple of 64: the operand index is wave-uniform
         const int e = tid + 256 * it, o = __builtin_amdgcn_readfirstlane(e / NB), blk = e - o * NB;
         const int rp = blk / DP, dp = blk - rp * DP;
-        const bool live = o < sa.nops && tile < sa.op[o < sa.nops ? o : 0].ntiles;
-        const SplitOp& op = sa.op[o < sa.nops ? o : 0];
-        const float* src = op.x + (int64_t)b * op.xs + h * hd;
-        const int64_t rs = (int64_t)sa.B * op.xs;
+        const int oi = o < sa.nops ? o : 0;
+        const float* xp = sa.op[oi].x;   // fields read once, up front
+        const int64_t xs = sa.op[oi].xs;
+        T_[it] = sa.op[oi].T;
+        ones_[it] = sa.op[oi].ones;
+        mul_[it] = sa.op[oi].mul;
+        live[it] = (o < sa.nops) & (tile < sa.op[oi].ntiles);
+        const float* src = xp + (int64_t)b * xs + h * hd;
+        const int64_t rs = (int64_t)sa.B * xs;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd)   // unconditional in-bounds loads, issued back to back
+                x[it][rr][dd] = src[(int64_t)min(tile * MT + 2 * rp + rr, T_[it] - 1) * rs + min(2 * dp + dd, hd - 1)];
+    }
+    // consume every loaded value here, so the compiler cannot sink a load under a branch below
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) asm volatile("" : "+v"(x[it][rr][dd]));
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = tid + 256 * it, o = __builtin_amdgcn_readfirstlane(e / NB), blk = e - o * NB;
+        const int rp = blk / DP, dp = blk - rp * DP;
+        (void)o;
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
             for (int dd = 0; dd < 2; ++dd) {
                 const int j = tile * MT + 2 * rp + rr, c = 2 * dp + dd;
-                float v = 0.f;
-                if (live && j < op.T) v = c < hd ? src[(int64_t)j * rs + c] * op.mul : (c == op.ones ? 1.f : 0.f);
-                x[it][rr][dd] = v;
+                const bool ok = live[it] & (j < T_[it]);
+                const float one = (ok & (c == ones_[it])) ? 1.f : 0.f;
+                x[it][rr][dd] = (ok & (c < hd)) ? x[it][rr][dd] * mul_[it] : one;
             }
     }
     float dl = 0.f;   // delta of row tid (backward)
@@ -208,8 +234,8 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
         float ov[HDP], gv[HDP];
 #pragma unroll
         for (int c = 0; c < HDP; ++c) {
-            ov[c] = c < hd ? sa.o[off + c] : 0.f;
-            gv[c] = c < hd ? sa.g[off + c] : 0.f;
+            ov[c] = sa.o[off + min(c, hd - 1)];
+            gv[c] = c < hd ? sa.g[off + min(c, hd - 1)] : 0.f;
         }
 #pragma unroll
         for (int c = 0; c < HDP; ++c) dl = fmaf(ov[c], gv[c], dl);
