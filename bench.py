@@ -367,6 +367,10 @@ def main():
                              "attention at head_dim 2/4 has no MFMA-shaped contraction and issues no MFMA",
                      "mfma": "f32 matrix-core roof (157.3 TF dense)",
                      "hbm": "HBM3E bandwidth roof (8 TB/s)"}
+            if dom_name.startswith("mha_"):
+                notes["mfma"] = ("fp32-class contractions on the bf16 matrix cores (three bf16 products per fp32 "
+                                 "product, ceiling 2500/3 = 833 TF); frac is against the 157.3 TF f32 roof of the "
+                                 "arithmetic type; algorithmic FLOPs count the full Tq x Tk square (4/10 T^2 E fwd/bwd)")
             roofline = dict(kernel=dom_name, bound=bound, achieved=round(achieved, 3), peak=peak, unit=unit,
                             frac=round(achieved / peak, 4), traffic=traffic,
                             avg_ms=round(dom["avg_ms"], 4), launches_per_step=dom["launches"] / steps_timed,
@@ -375,6 +379,13 @@ def main():
                             algorithmic_gbs=round(gbs, 1), algorithmic_tflops=round(tflops, 3),
                             note=notes[bound] + "; traffic (HBM bytes per launch, PMC) from " +
                             (pmc_file or "no PMC summary yet"))
+            if dom_name.startswith("mha_"):
+                # causal mask (diag 1, Tq = Tk = T): (T + 1) / (2T) of the square is visible
+                T = (args.size // 8) ** 3
+                useful = (T + 1) / (2.0 * T)
+                roofline.update(causal_useful_fraction=round(useful, 4),
+                                useful_tflops=round(tflops * useful, 3),
+                                useful_frac=round(tflops * useful / FP32_PEAK_TFLOPS, 4))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
