@@ -149,36 +149,42 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
     // key n), a cross-lane order the compiler cannot see, so a compiler barrier after each key's
     // table stores keeps every later table read behind them (LDS executes a wave's accesses in
     // order; no wait is needed).
+    // Keys are walked row by row (a row = WW consecutive keys, fixed (i, j)).  Per row one uniform
+    // base addresses the broadcast K/V records and one lane base the table entries, so every
+    // per-key access below is a base register plus an immediate offset (no per-key address math):
+    // record of key n at kv2[8 n] (k c0, k c1, v c0, v c1 of key n, then of key n + H); entries of
+    // key k of the row at trow + (WW - 1 - k) EB, trow = lane_base - (code0 + WW - 1) EB.
     f2 kk[2][2], vv[2][2], tbm, tb0, tbp;
-    auto fetch = [&](int nn, int code, f2 (&k_)[2][2], f2 (&v_)[2][2], f2& m_, f2& z_, f2& p_) {
+    auto fetch = [&](const f2* kvk, const char* pe, f2 (&k_)[2][2], f2 (&v_)[2][2], f2& m_, f2& z_, f2& p_) {
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                k_[v][c] = kv2[(v * 4 + c) * Wn::H + nn];
-                v_[v][c] = kv2[(v * 4 + 2 + c) * Wn::H + nn];
+                k_[v][c] = kvk[v * 4 + c];
+                v_[v][c] = kvk[v * 4 + 2 + c];
             }
-        const char* pm = tb + (lane_base - (uint32_t)(code * EB));
-        m_ = *reinterpret_cast<const f2*>(pm);
-        z_ = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
-        p_ = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
+        m_ = *reinterpret_cast<const f2*>(pe);
+        z_ = *reinterpret_cast<const f2*>(pe + Wn::DC * EB);
+        p_ = *reinterpret_cast<const f2*>(pe + 2 * Wn::DC * EB);
     };
-    fetch(0, 0, kk, vv, tbm, tb0, tbp);
-    int n = 0;
+    fetch(kv2, tb + lane_base, kk, vv, tbm, tb0, tbp);
     for (int i = 0; i < WD / 2; ++i) {
         for (int j = 0; j < WH; ++j) {
+            const int code0 = i * Wn::TW + j * Wn::TH;
+            const f2* kvr = kv2 + (i * WH + j) * WW * 8;
+            char* trow = tb + (lane_base - (uint32_t)((code0 + WW - 1) * EB));
+            // the next row's bases, for the prefetch at the row's last key (the final row re-reads
+            // itself: valid, unused data)
+            const int jn = j + 1 < WH ? j + 1 : 0, in = j + 1 < WH ? i : i + 1;
+            const bool last = in == WD / 2;
+            const f2* kvn = last ? kvr : kv2 + (in * WH + jn) * WW * 8;
+            const char* pen = last ? trow : tb + (lane_base - (uint32_t)((in * Wn::TW + jn * Wn::TH) * EB));
 #pragma unroll
-            for (int k = 0; k < WW; ++k, ++n) {
-                const int code = i * Wn::TW + j * Wn::TH + k;
-                char* pm = tb + (lane_base - (uint32_t)(code * EB));   // entry E-  (query t, key n + H)
-                // next key's rows and bias entries (the last fetch of the loop reads valid, unused data)
-                const int k1 = k + 1 < WW ? k + 1 : 0;
-                const int j1 = k + 1 < WW ? j : (j + 1 < WH ? j + 1 : 0);
-                const int i1 = (k + 1 < WW || j + 1 < WH) ? i : i + 1;
-                const int n1 = n + 1 < Wn::H ? n + 1 : n;
-                const int code1 = n + 1 < Wn::H ? i1 * Wn::TW + j1 * Wn::TH + k1 : code;
+            for (int k = 0; k < WW; ++k) {
+                char* pm = trow + (WW - 1 - k) * EB;   // entry E-  (query t, key n + H)
                 f2 nk[2][2], nv[2][2], nm, nz, np;
-                fetch(n1, code1, nk, nv, nm, nz, np);
+                if (k + 1 < WW) fetch(kvr + (k + 1) * 8, trow + (WW - 2 - k) * EB, nk, nv, nm, nz, np);
+                else fetch(kvn, pen, nk, nv, nm, nz, np);
                 // this key's table-gradient entries (after the previous key's stores)
                 f2* dm = reinterpret_cast<f2*>(pm + DTO);
                 f2* d0 = reinterpret_cast<f2*>(pm + Wn::DC * EB + DTO);
@@ -233,7 +239,7 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
     const WGeom& g = a.g;
     const int NHG = a.hsplit, NHT = 2 * NHG;
     float* tabdt = smem;                          // [3][TSZ] f2: bias pair, dt wave 0, dt wave 1
-    float* kv_s = tabdt + TSZ * 6;                // [8][kSA] f2: k c0, k c1, v c0, v c1 of keys n, then n + H
+    float* kv_s = tabdt + TSZ * 6;                // [H][8] f2: k c0, k c1, v c0, v c1 of key n, then of n + H
     const bc::Items it = bc::items(NHG);
     const int tid = threadIdx.x, wave = tid >> 6;
     const bool lane_ok = tid < H;
@@ -269,11 +275,11 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
                 q[u].x[1] *= qscale;
                 ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
                 lse2[u] = (f2){a.lse[ti.row * NHT + 2 * it.hp], a.lse[ti.row * NHT + 2 * it.hp + 1]} * kLog2e;
-                f2* kv2 = reinterpret_cast<f2*>(kv_s) + u * 4 * Wn::H + t;
+                f2* kv2 = reinterpret_cast<f2*>(kv_s) + t * 8 + u * 4;   // key record t
                 kv2[0] = (f2){kr.x, kr.z};
-                kv2[Wn::H] = (f2){kr.y, kr.w};
-                kv2[2 * Wn::H] = (f2){vr.x, vr.z};
-                kv2[3 * Wn::H] = (f2){vr.y, vr.w};
+                kv2[1] = (f2){kr.y, kr.w};
+                kv2[2] = (f2){vr.x, vr.z};
+                kv2[3] = (f2){vr.y, vr.w};
                 dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
             }
         }
@@ -315,24 +321,27 @@ __device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2]
     // entry of (query n, key t) = code(n) + ck, ck = OFF - code(t); (n, t + H) is DC lower,
     // (n + H, t) DC higher
     const uint32_t lane_base = (uint32_t)((ck - Wn::DC) * EB);
+    // query records rs2[12 n]: q2 c0, q2 c1, dO c0, dO c1, lse2, -delta of query n, then of n + H;
+    // per row one base each for the records and the table entries, immediates per query
     const f2* rs2 = reinterpret_cast<const f2*>(rs_s);
-    int n = 0;
     for (int i = 0; i < WD / 2; ++i) {
         for (int j = 0; j < WH; ++j) {
-#pragma unroll
-            for (int k = 0; k < WW; ++k, ++n) {
-                const int code = i * Wn::TW + j * Wn::TH + k;
-                const char* pm = tb + (lane_base + (uint32_t)(code * EB));   // (n, t + H)
+            const int code0 = i * Wn::TW + j * Wn::TH;
+            const f2* rsr = rs2 + (i * WH + j) * WW * 12;
+            const char* trow = tb + (lane_base + (uint32_t)(code0 * EB));
+#pragma unroll 3   // fully unrolled, the hoisted record loads spill at the 3-wave budget
+            for (int k = 0; k < WW; ++k) {
+                const char* pm = trow + k * EB;   // (n, t + H)
                 f2 qq[2][2], gg[2][2], ls[2], nd[2];
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
-                    const f2* src = rs2 + u * 6 * Wn::H + n;
+                    const f2* src = rsr + k * 12 + u * 6;
                     qq[u][0] = src[0];
-                    qq[u][1] = src[Wn::H];
-                    gg[u][0] = src[2 * Wn::H];
-                    gg[u][1] = src[3 * Wn::H];
-                    ls[u] = src[4 * Wn::H];
-                    nd[u] = src[5 * Wn::H];
+                    qq[u][1] = src[1];
+                    gg[u][0] = src[2];
+                    gg[u][1] = src[3];
+                    ls[u] = src[4];
+                    nd[u] = src[5];
                 }
                 const f2 tbm = *reinterpret_cast<const f2*>(pm);
                 const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
@@ -375,7 +384,7 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
     const WGeom& g = a.g;
     const int NHG = a.hsplit, NHT = 2 * NHG;
     float* tab_s = smem;                            // [TSZ][2] bias * log2e of the head pair
-    float* rs_s = tab_s + TSZ * 2;                  // [12][kSA] f2: q2 c0, q2 c1, dO c0, dO c1, lse2, -delta
+    float* rs_s = tab_s + TSZ * 2;                  // [H][12] f2: q2 c0, q2 c1, dO c0, dO c1, lse2, -delta
     const bc::Items it = bc::items(NHG);
     const int tid = threadIdx.x;
     const bool lane_ok = tid < H;
@@ -404,14 +413,14 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
                 const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti.row * a.os + coff);
                 const float4 orow = *reinterpret_cast<const float4*>(a.o + ti.row * a.os + coff);
                 const float l0 = a.lse[ti.row * NHT + 2 * it.hp], l1 = a.lse[ti.row * NHT + 2 * it.hp + 1];
-                f2* dst = reinterpret_cast<f2*>(rs_s) + u * 6 * Wn::H + t;
+                f2* dst = reinterpret_cast<f2*>(rs_s) + t * 12 + u * 6;   // query record t
                 const float d0 = orow.x * gr.x + orow.y * gr.y, d1 = orow.z * gr.z + orow.w * gr.w;
                 dst[0] = (f2){qr.x * qs2, qr.z * qs2};
-                dst[Wn::H] = (f2){qr.y * qs2, qr.w * qs2};
-                dst[2 * Wn::H] = (f2){gr.x, gr.z};
-                dst[3 * Wn::H] = (f2){gr.y, gr.w};
-                dst[4 * Wn::H] = (f2){l0 * kLog2e, l1 * kLog2e};
-                dst[5 * Wn::H] = (f2){-d0, -d1};
+                dst[1] = (f2){qr.y * qs2, qr.w * qs2};
+                dst[2] = (f2){gr.x, gr.z};
+                dst[3] = (f2){gr.y, gr.w};
+                dst[4] = (f2){l0 * kLog2e, l1 * kLog2e};
+                dst[5] = (f2){-d0, -d1};
             }
         }
         __syncthreads();
