@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 4
+#define MMNI_ABI_VERSION 5
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -115,7 +115,9 @@ int mmni_relative_index(const mmni_wattn_desc* d, int32_t* idx, void* stream);
  * Time-major layout (T, B, E): element (t, b, h, c) at ptr[(t*B + b)*stride + h*head_dim + c].
  * head_dim 1..16, padded to 4 / 8 / 16.  The contractions run on the bf16 matrix cores with each
  * fp32 operand split into bf16 hi + lo and three products (hi*hi + hi*lo + lo*hi) accumulated in
- * fp32: ~2^-16 relative error per product, fp32-class results.
+ * fp32: ~2^-16 relative error per product, fp32-class results.  With dtype = 1 (bf16 storage,
+ * SURVEY §8d C5) the operands are bf16 already and one product is taken (fp32 accumulation and
+ * softmax; the probabilities enter P·V rounded to bf16).
  * Attention dropout (multihead_attention.py:123, F.dropout of the probabilities): dropout = p in
  * [0, 1); element (b, h, i, j) is kept iff a counter-based hash of (seed, (b*heads + h)*Tq + i, j)
  * falls below (1 - p) * 2^32, and kept probabilities are scaled by 1 / (1 - p).  The same seed in
@@ -132,20 +134,22 @@ typedef struct mmni_mha_desc {
     int64_t q_stride, k_stride, v_stride, o_stride;
     float   dropout;            /* attention-probability dropout p (0: none)              */
     uint32_t seed;              /* dropout stream; forward and backward must agree         */
+    int32_t dtype;              /* storage of q/k/v/out/dout/dq/dk/dv: 0 fp32, 1 bf16 (ABI v5);
+                                   lse and the softmax are fp32 either way                   */
 } mmni_mha_desc;
 
 size_t mmni_mha_fwd_workspace_bytes(const mmni_mha_desc* d);
 size_t mmni_mha_bwd_workspace_bytes(const mmni_mha_desc* d);
 /* out: (Tq, B, E) rows with o_stride; lse: (B, heads, Tq) of the undropped softmax. */
-int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                 float* out, float* lse, void* workspace, void* stream);
+int mmni_mha_fwd(const mmni_mha_desc* d, const void* q, const void* k, const void* v,
+                 void* out, float* lse, void* workspace, void* stream);
 /* dq/dk/dv overwritten. */
-int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                 const float* out, const float* dout, const float* lse,
-                 float* dq, float* dk, float* dv, void* workspace, void* stream);
+int mmni_mha_bwd(const mmni_mha_desc* d, const void* q, const void* k, const void* v,
+                 const void* out, const void* dout, const float* lse,
+                 void* dq, void* dk, void* dv, void* workspace, void* stream);
 /* Head-averaged (dropped) attention probabilities (B, Tq, Tk) — the second return value of
  * MultiheadAttention.forward (multihead_attention.py:131-133). */
-int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const float* k,
+int mmni_mha_mean_probs(const mmni_mha_desc* d, const void* q, const void* k,
                         const float* lse, float* probs, void* stream);
 /* The dropout multipliers (0 or 1/(1-p)) of every (b, h, i, j) as (B, heads, Tq, Tk) floats:
  * the mask the forward and backward apply, exported for tests. */

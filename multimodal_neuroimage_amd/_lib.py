@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -36,7 +36,7 @@ class MhaDesc(ctypes.Structure):
     _fields_ = [("Tq", _c_i32), ("Tk", _c_i32), ("B", _c_i32), ("heads", _c_i32), ("head_dim", _c_i32),
                 ("causal_diag", _c_i32), ("scale", _c_f),
                 ("q_stride", _c_i64), ("k_stride", _c_i64), ("v_stride", _c_i64), ("o_stride", _c_i64),
-                ("dropout", _c_f), ("seed", ctypes.c_uint32)]
+                ("dropout", _c_f), ("seed", ctypes.c_uint32), ("dtype", ctypes.c_int32)]
 
 
 class Conv3dDesc(ctypes.Structure):
@@ -142,12 +142,12 @@ def ptr(t):
     return _vp(t.data_ptr()) if t is not None else _vp(0)
 
 
-def require_device(*tensors, what="mmni"):
+def require_device(*tensors, what="mmni", dtypes=(torch.float32,)):
     for t in tensors:
         if t is None:
             continue
         if not t.is_cuda:
             raise RuntimeError(f"{what}: tensors must live on a ROCm device (got {t.device}); "
                                "the HIP hot path has no CPU fallback")
-        if t.dtype != torch.float32:
-            raise RuntimeError(f"{what}: expected float32 tensors, got {t.dtype}")
+        if t.dtype not in dtypes:
+            raise RuntimeError(f"{what}: expected {' or '.join(str(d) for d in dtypes)} tensors, got {t.dtype}")

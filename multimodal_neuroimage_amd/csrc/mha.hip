@@ -36,6 +36,7 @@
 // --attn_dropout 0.1, main.py:176): counter-based, keep(b*h, i, j) = hash(seed, (b*h)*Tq + i, j)
 // < (1 - p) * 2^32, regenerated identically in the backward and by mmni_mha_dropout_mask.
 #include "mmni_common.h"
+#include <type_traits>
 
 namespace mmni {
 
@@ -48,6 +49,18 @@ __device__ __forceinline__ mf4 mfma_bf(u4 a, u4 b, mf4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
 }
+
+// element I/O: fp32 or bf16 storage, fp32 arithmetic
+template <typename T>
+__device__ __forceinline__ float ldf(const void* p, int64_t i) {
+    return (float)static_cast<const T*>(p)[i];
+}
+template <typename T>
+__device__ __forceinline__ void stf(void* p, int64_t i, float v) {
+    static_cast<T*>(p)[i] = (T)v;
+}
+template <typename T>
+constexpr int kTerms = std::is_same<T, float>::value ? 3 : 1;   // bf16 products per fp32 product
 
 // bf16 split of fp32: hi = truncation (exact as an fp32), lo = round(x - hi)
 __device__ __forceinline__ float bf_hi(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
@@ -67,22 +80,23 @@ struct MhaArgs {
     float scale;
     float scale2;                   // scale * log2(e)
     int64_t qs, ks, vs, os;
-    const float* q;
-    const float* k;
-    const float* v;
-    float* out;
+    const void* q;                  // q / k / v / o / dout / out / dq / dk / dv: fp32 or bf16 (dtype)
+    const void* k;
+    const void* v;
+    void* out;
     float* lse;                     // (B, H, Tq) natural log
-    const float* o;
-    const float* dout;
-    float* dq;
-    float* dk;
-    float* dv;
+    const void* o;
+    const void* dout;
+    void* dq;
+    void* dk;
+    void* dv;
     float* delta;                   // (B, H, Tq)
     float* probs;                   // (B, Tq, Tk)
     float inv_keep;                 // 1 / (1 - p)
     uint32_t thresh;                // keep iff hash < thresh
     uint32_t seed;
     int nqt, nkt;                   // 64-row tiles of the query / key sequences
+    int bf16;                       // element type of q/k/v/o/dout and of the outputs
     // bf16 split images in the workspace (mha_split_kernel), [bh][tile][...]
     const uint16_t* kx;             // K ext
     const uint16_t* kz;             // K Z
@@ -97,13 +111,15 @@ struct MhaArgs {
 constexpr int MT = 64;      // rows per LDS tile and per workgroup (4 waves x 16)
 
 // LDS image geometry per padded head_dim
-template <int HDP>
+// TERMS = 3 (fp32 data: hi/lo split, three products) or 1 (bf16 data: one product)
+template <int HDP, int TERMS = 3>
 struct Geo {
-    static constexpr int NX = (3 * HDP + 31) / 32;   // S-type MFMAs per 16 x 16 sub-tile
+    static constexpr int NX = (TERMS * HDP + 31) / 32;   // S-type MFMAs per 16 x 16 sub-tile
     static constexpr int XS = 32 * NX + 8;           // ext image row stride (bf16): 80 / 144 B, conflict-free
-    static constexpr bool RS = HDP <= 8;             // Z image: row-split (one MFMA per 16 rows)
+    static constexpr bool RS = TERMS == 3 && HDP <= 8;   // Z image: row-split (one MFMA per 16 rows)
     static constexpr int ZS = RS ? 136 : 72;         // Z image row stride (bf16): 272 / 144 B
-    static constexpr int ZR = RS ? 16 : 32;          // Z image rows (RS: hi 0-7, lo 8-15; else hi 0-15, lo 16-31)
+    // Z image rows (RS: hi 0-7, lo 8-15; 3 terms, d = 16: hi 0-15, lo 16-31; 1 term: 0-15)
+    static constexpr int ZR = TERMS == 1 ? 16 : (RS ? 16 : 32);
     static constexpr int EW = 32 * NX;               // ext image row in global (unpadded)
     static constexpr int ZW = RS ? 128 : 64;         // Z image row in global (unpadded)
     static constexpr int XT = MT * EW;               // ext tile (bf16 elements)
@@ -137,8 +153,9 @@ __device__ __forceinline__ int key_end(const MhaArgs& a, int i) {
 // short tiles interleave in dispatch order (even load per CU)
 __device__ __forceinline__ int zigzag(int x, int n) { return (x & 1) ? n - 1 - (x >> 1) : (x >> 1); }
 
-__device__ __forceinline__ float load_pad(const float* base, int64_t rowoff, int c, int hd, bool ok) {
-    return (ok && c < hd) ? base[rowoff + c] : 0.f;
+template <typename T>
+__device__ __forceinline__ float load_pad(const void* base, int64_t rowoff, int c, int hd, bool ok) {
+    return (ok && c < hd) ? ldf<T>(base, rowoff + c) : 0.f;
 }
 
 // ------------------------------------------------------------------------------------
@@ -147,7 +164,7 @@ __device__ __forceinline__ float load_pad(const float* base, int64_t rowoff, int
 // A operand, see Geo).  The attention kernels then stage a tile with 16-byte copies.
 // ------------------------------------------------------------------------------------
 struct SplitOp {
-    const float* x;     // (T, B, stride) time-major, head h at column h * hd
+    const void* x;      // (T, B, stride) time-major, head h at column h * hd (fp32 or bf16)
     int64_t xs;         // row stride of (t, b)
     int T, ntiles;
     float mul;
@@ -160,8 +177,8 @@ struct SplitArgs {
     int nops;
     int B, H, hd;
     // delta = rowsum(dO * O) as the last z-slice (backward): o/g rows with stride os
-    const float* o;
-    const float* g;
+    const void* o;
+    const void* g;
     int64_t os;
     int Tq;
     float* delta;       // (B, H, Tq)
@@ -170,9 +187,10 @@ struct SplitArgs {
 // grid (tiles, B * H): a block builds the 64-row tile images of one head for every operand in LDS
 // (all operands' loads in flight together), adds the delta rows of the tile (backward), then
 // writes the images out with coalesced 16-byte stores
-template <int HDP>
+template <int HDP, typename T>
 __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
-    using G = Geo<HDP>;
+    constexpr int TERMS = kTerms<T>;
+    using G = Geo<HDP, TERMS>;
     constexpr int IMG = G::XT + G::ZT;
     __shared__ __attribute__((aligned(16))) uint16_t img[4 * IMG];
     const int tile = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, hd = sa.hd, H = sa.H;
@@ -190,19 +208,19 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
         const int e = tid + 256 * it, o = __builtin_amdgcn_readfirstlane(e / NB), blk = e - o * NB;
         const int rp = blk / DP, dp = blk - rp * DP;
         const int oi = o < sa.nops ? o : 0;
-        const float* xp = sa.op[oi].x;   // fields read once, up front
+        const T* xp = static_cast<const T*>(sa.op[oi].x);   // fields read once, up front
         const int64_t xs = sa.op[oi].xs;
         T_[it] = sa.op[oi].T;
         ones_[it] = sa.op[oi].ones;
         mul_[it] = sa.op[oi].mul;
         live[it] = (o < sa.nops) & (tile < sa.op[oi].ntiles);
-        const float* src = xp + (int64_t)b * xs + h * hd;
+        const T* src = xp + (int64_t)b * xs + h * hd;
         const int64_t rs = (int64_t)sa.B * xs;
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
             for (int dd = 0; dd < 2; ++dd)   // unconditional in-bounds loads, issued back to back
-                x[it][rr][dd] = src[(int64_t)min(tile * MT + 2 * rp + rr, T_[it] - 1) * rs + min(2 * dp + dd, hd - 1)];
+                x[it][rr][dd] = (float)src[(int64_t)min(tile * MT + 2 * rp + rr, T_[it] - 1) * rs + min(2 * dp + dd, hd - 1)];
     }
     // consume every loaded value here, so the compiler cannot sink a load under a branch below
 #pragma unroll
@@ -234,8 +252,8 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
         float ov[HDP], gv[HDP];
 #pragma unroll
         for (int c = 0; c < HDP; ++c) {
-            ov[c] = sa.o[off + min(c, hd - 1)];
-            gv[c] = c < hd ? sa.g[off + min(c, hd - 1)] : 0.f;
+            ov[c] = ldf<T>(sa.o, off + min(c, hd - 1));
+            gv[c] = c < hd ? ldf<T>(sa.g, off + min(c, hd - 1)) : 0.f;
         }
 #pragma unroll
         for (int c = 0; c < HDP; ++c) dl = fmaf(ov[c], gv[c], dl);
@@ -254,6 +272,10 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
                 const int w = ((r + rr) * G::EW + d) >> 1;
+                if (TERMS == 1) {   // [x | 0]
+                    xw[w] = pk_rn(x[it][rr][0], x[it][rr][1]);
+                    continue;
+                }
                 const uint32_t hi = pk_hi(x[it][rr][0], x[it][rr][1]);
                 xw[w] = hi;
                 xw[w + HDP / 2] = hi;
@@ -263,6 +285,12 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
         if (op.z) {
 #pragma unroll
             for (int dd = 0; dd < 2; ++dd) {
+                if (TERMS == 1) {   // [d][c][lg][j], one term
+                    const int j = ((r >> 4) & 1) * 4 + (r & 3);
+                    const int w = ((d + dd) * G::ZW + (r >> 5) * 32 + ((r & 15) >> 2) * 8 + j) >> 1;
+                    zw[w] = pk_rn(x[it][0][dd], x[it][1][dd]);
+                    continue;
+                }
                 const uint32_t hi = pk_hi(x[it][0][dd], x[it][1][dd]), lo = pk_lo(x[it][0][dd], x[it][1][dd]);
                 if (G::RS) {   // [m][st][lg][j]: m < 8 hi (j and j + 4), m >= 8 lo (j < 4)
                     const int w = ((d + dd) * G::ZW + (r >> 4) * 32 + ((r & 15) >> 2) * 8 + (r & 3)) >> 1;
@@ -324,10 +352,10 @@ struct TileCopy {
 
 
 // register-side ext vector [hi | lo | hi | 0] of this lane's row (v = the row, HDP floats)
-template <int HDP>
-__device__ __forceinline__ void build_y(const float (&v)[HDP], int lg, u4 (&y)[Geo<HDP>::NX]) {
+template <int HDP, int TERMS>
+__device__ __forceinline__ void build_y(const float (&v)[HDP], int lg, u4 (&y)[Geo<HDP, TERMS>::NX]) {
 #pragma unroll
-    for (int c = 0; c < Geo<HDP>::NX; ++c)
+    for (int c = 0; c < Geo<HDP, TERMS>::NX; ++c)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
             const int e = 32 * c + 8 * lg + 2 * jj;
@@ -338,15 +366,16 @@ __device__ __forceinline__ void build_y(const float (&v)[HDP], int lg, u4 (&y)[G
                 x0 = t == d ? v[t] : x0;
                 x1 = t == d + 1 ? v[t] : x1;
             }
-            y[c][jj] = (seg == 0 || seg == 2) ? pk_hi(x0, x1) : (seg == 1 ? pk_lo(x0, x1) : 0u);
+            if (TERMS == 1) y[c][jj] = seg == 0 ? pk_rn(x0, x1) : 0u;
+            else y[c][jj] = (seg == 0 || seg == 2) ? pk_hi(x0, x1) : (seg == 1 ? pk_lo(x0, x1) : 0u);
         }
 }
 
 // S-type: acc += X[16 st + (lane & 15)][:] . Y[:]  over the 3-term ext dimension
-template <int HDP>
-__device__ __forceinline__ mf4 sprod(const uint16_t* xe, int st, const u4 (&y)[Geo<HDP>::NX], mf4 acc, int ln,
-                                     int lg) {
-    using G = Geo<HDP>;
+template <int HDP, int TERMS>
+__device__ __forceinline__ mf4 sprod(const uint16_t* xe, int st, const u4 (&y)[Geo<HDP, TERMS>::NX], mf4 acc,
+                                     int ln, int lg) {
+    using G = Geo<HDP, TERMS>;
 #pragma unroll
     for (int c = 0; c < G::NX; ++c)
         acc = mfma_bf(*reinterpret_cast<const u4*>(xe + (16 * st + ln) * G::XS + 32 * c + 8 * lg), y[c], acc);
@@ -354,10 +383,17 @@ __device__ __forceinline__ mf4 sprod(const uint16_t* xe, int st, const u4 (&y)[G
 }
 
 // Z-type: acc(d x cols) += Z^T(d x 64 rows) . W(64 rows x cols), W in accumulator layout
-template <int HDP>
+template <int HDP, int TERMS>
 __device__ __forceinline__ mf4 zprod(const uint16_t* z, const mf4 (&w)[4], mf4 acc, int ln, int lg) {
-    using G = Geo<HDP>;
-    if constexpr (G::RS) {
+    using G = Geo<HDP, TERMS>;
+    if constexpr (TERMS == 1) {   // one MFMA per 32 rows, W rounded to bf16
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const mf4 &wa = w[2 * c], &wb = w[2 * c + 1];
+            const u4 B = {pk_rn(wa[0], wa[1]), pk_rn(wa[2], wa[3]), pk_rn(wb[0], wb[1]), pk_rn(wb[2], wb[3])};
+            acc = mfma_bf(*reinterpret_cast<const u4*>(z + ln * G::ZS + c * 32 + lg * 8), B, acc);
+        }
+    } else if constexpr (G::RS) {
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
             const u4 A = *reinterpret_cast<const u4*>(z + ln * G::ZS + st * 32 + lg * 8);
@@ -382,16 +418,16 @@ __device__ __forceinline__ mf4 zprod(const uint16_t* z, const mf4 (&w)[4], mf4 a
 }
 
 // the Z-type result: row-split halves summed (rows d = 4 (lg & 1) + i then), else rows d = 4 lg + i
-template <int HDP>
+template <int HDP, int TERMS>
 __device__ __forceinline__ mf4 zfinish(mf4 acc) {
-    if constexpr (Geo<HDP>::RS) {
+    if constexpr (Geo<HDP, TERMS>::RS) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i] += __shfl_xor(acc[i], 32);
     }
     return acc;
 }
-template <int HDP>
-__device__ __forceinline__ bool zrow_owner(int lg) { return Geo<HDP>::RS ? lg < 2 : true; }
+template <int HDP, int TERMS>
+__device__ __forceinline__ bool zrow_owner(int lg) { return Geo<HDP, TERMS>::RS ? lg < 2 : true; }
 
 // S^T tile of a query-row wave (lane: keys k0 + 16 st + 4 lg + i, query qi): -inf past Tk and
 // under the causal mask (selects, no branches)
@@ -446,9 +482,10 @@ __device__ __forceinline__ void tile_loop(int tb, int te, Load&& load, Store&& s
 // ------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
-    using G = Geo<HDP>;
+    constexpr int TERMS = kTerms<T>;
+    using G = Geo<HDP, TERMS>;
     constexpr int SK = MT * G::XS, SV = G::ZR * G::ZS, STAGE = SK + SV;   // K ext + V Z
     constexpr int NBUF = Stages<STAGE * 2>::N;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * STAGE];
@@ -463,8 +500,8 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
         float qv[HDP];
         const int64_t rq = ((int64_t)qi * a.B + b) * a.qs + h * a.hd;
 #pragma unroll
-        for (int d = 0; d < HDP; ++d) qv[d] = load_pad(a.q, rq, d, a.hd, qok) * a.scale2;
-        build_y<HDP>(qv, lg, qy);
+        for (int d = 0; d < HDP; ++d) qv[d] = load_pad<T>(a.q, rq, d, a.hd, qok) * a.scale2;
+        build_y<HDP, TERMS>(qv, lg, qy);
     }
     const bool ones = !DROP && a.hd < HDP;   // the denominator as V's padding row of ones (host sets it)
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
@@ -493,7 +530,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
             const uint16_t* vz = kx + SK;
             mf4 s[4];
 #pragma unroll
-            for (int st = 0; st < 4; ++st) s[st] = sprod<HDP>(kx, st, qy, (mf4){0.f, 0.f, 0.f, 0.f}, ln, lg);
+            for (int st = 0; st < 4; ++st) s[st] = sprod<HDP, TERMS>(kx, st, qy, (mf4){0.f, 0.f, 0.f, 0.f}, ln, lg);
             // lane: s[st][i] = S^T[key k0 + 16 st + 4 lg + i][query qi] (log2 domain)
             const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
             if (edge) mask_keys(s, k0, qi, lg, a);
@@ -521,9 +558,9 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
                     s[st][i] = pv;
                 }
             }
-            o = zprod<HDP>(vz, s, o, ln, lg);
+            o = zprod<HDP, TERMS>(vz, s, o, ln, lg);
         });
-    o = zfinish<HDP>(o);
+    o = zfinish<HDP, TERMS>(o);
     if (ones) {
         const int hd = a.hd, src = ((hd >> 2) << 4) + ln, i = hd & 3;
         const float t = i == 0 ? o[0] : (i == 1 ? o[1] : (i == 2 ? o[2] : o[3]));
@@ -534,12 +571,12 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     }
     if (qok) {
         const float inv = 1.0f / lsum;
-        float* orow = a.out + ((int64_t)qi * a.B + b) * a.os + h * a.hd;
-        if (zrow_owner<HDP>(lg)) {
+        const int64_t orow = ((int64_t)qi * a.B + b) * a.os + h * a.hd;
+        if (zrow_owner<HDP, TERMS>(lg)) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
-                if (d < a.hd) orow[d] = o[i] * inv;
+                if (d < a.hd) stf<T>(a.out, orow + d, o[i] * inv);
             }
         }
         if (lg == 0) a.lse[(int64_t)bh * a.Tq + qi] = (m + fast_log2(lsum)) * kLn2;
@@ -549,18 +586,20 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
 // ------------------------------------------------------------------------------------
 // dq: wave = 16 queries, loops over key tiles
 // ------------------------------------------------------------------------------------
-template <int HDP>
+template <int HDP, int TERMS>
 struct DqLds {
-    using G = Geo<HDP>;
+    using G = Geo<HDP, TERMS>;
     static constexpr int SX = MT * G::XS, SZ = G::ZR * G::ZS, STAGE = 2 * SX + SZ;   // K ext, V ext, K Z
     static constexpr int NBUF = Stages<STAGE * 2>::N;
     static constexpr int BYTES = NBUF * STAGE * 2;
 };
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int bx) {
-    using G = Geo<HDP>;
-    constexpr int SX = DqLds<HDP>::SX, SZ = DqLds<HDP>::SZ, STAGE = DqLds<HDP>::STAGE;
-    constexpr int NBUF = DqLds<HDP>::NBUF;
+    constexpr int TERMS = kTerms<T>;
+    using G = Geo<HDP, TERMS>;
+    using L = DqLds<HDP, TERMS>;
+    constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
+    constexpr int NBUF = L::NBUF;
     (void)SZ;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
@@ -573,11 +612,11 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
         float qv[HDP], gv[HDP];
 #pragma unroll
         for (int d = 0; d < HDP; ++d) {
-            qv[d] = load_pad(a.q, rq, d, a.hd, qok) * a.scale2;
-            gv[d] = load_pad(a.dout, ro, d, a.hd, qok);
+            qv[d] = load_pad<T>(a.q, rq, d, a.hd, qok) * a.scale2;
+            gv[d] = load_pad<T>(a.dout, ro, d, a.hd, qok);
         }
-        build_y<HDP>(qv, lg, qy);
-        build_y<HDP>(gv, lg, gy);
+        build_y<HDP, TERMS>(qv, lg, qy);
+        build_y<HDP, TERMS>(gv, lg, gy);
     }
     const float lse2 = qok ? a.lse[(int64_t)bh * a.Tq + qi] * kLog2e : INFINITY;
     const float dl = qok ? a.delta[(int64_t)bh * a.Tq + qi] : 0.f;
@@ -615,8 +654,8 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
             mf4 s[4], dp[4];
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
-                s[st] = sprod<HDP>(kx, st, qy, sinit, ln, lg);    // S^T - lse2
-                dp[st] = sprod<HDP>(vx, st, gy, dinit, ln, lg);   // dP^T (- delta)
+                s[st] = sprod<HDP, TERMS>(kx, st, qy, sinit, ln, lg);    // S^T - lse2
+                dp[st] = sprod<HDP, TERMS>(vx, st, gy, dinit, ln, lg);   // dP^T (- delta)
             }
             const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
             if (edge) mask_keys(s, k0, qi, lg, a);
@@ -631,15 +670,14 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
                     s[st][i] = p * g;   // dS^T
                 }
             }
-            dq = zprod<HDP>(kz, s, dq, ln, lg);   // dQ^T += K^T dS^T
+            dq = zprod<HDP, TERMS>(kz, s, dq, ln, lg);   // dQ^T += K^T dS^T
         });
-    dq = zfinish<HDP>(dq);
-    if (qok && zrow_owner<HDP>(lg)) {
-        float* drow = a.dq + rq;
+    dq = zfinish<HDP, TERMS>(dq);
+    if (qok && zrow_owner<HDP, TERMS>(lg)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
-            if (d < a.hd) drow[d] = dq[i] * a.scale;
+            if (d < a.hd) stf<T>(a.dq, rq + d, dq[i] * a.scale);
         }
     }
 }
@@ -647,19 +685,21 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
 // ------------------------------------------------------------------------------------
 // dk, dv: wave = 16 keys, loops over query tiles
 // ------------------------------------------------------------------------------------
-template <int HDP>
+template <int HDP, int TERMS>
 struct DkvLds {
-    using G = Geo<HDP>;
+    using G = Geo<HDP, TERMS>;
     static constexpr int SX = MT * G::XS, SZ = G::ZR * G::ZS;
     static constexpr int STAGE = 2 * SX + 2 * SZ + 4 * MT;   // Q ext, dO ext, Q Z, dO Z, -lse2 and -delta (fp32)
     static constexpr int NBUF = Stages<STAGE * 2>::N;
     static constexpr int BYTES = NBUF * STAGE * 2;
 };
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, int bx) {
-    using G = Geo<HDP>;
-    constexpr int SX = DkvLds<HDP>::SX, SZ = DkvLds<HDP>::SZ, STAGE = DkvLds<HDP>::STAGE;
-    constexpr int NBUF = DkvLds<HDP>::NBUF;
+    constexpr int TERMS = kTerms<T>;
+    using G = Geo<HDP, TERMS>;
+    using L = DkvLds<HDP, TERMS>;
+    constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
+    constexpr int NBUF = L::NBUF;
     const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
     const int j0 = bx * MT + wave * 16;
@@ -671,11 +711,11 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
         float kv[HDP], vv[HDP];
 #pragma unroll
         for (int d = 0; d < HDP; ++d) {
-            kv[d] = load_pad(a.k, rk, d, a.hd, kok);
-            vv[d] = load_pad(a.v, rv, d, a.hd, kok);
+            kv[d] = load_pad<T>(a.k, rk, d, a.hd, kok);
+            vv[d] = load_pad<T>(a.v, rv, d, a.hd, kok);
         }
-        build_y<HDP>(kv, lg, ky);
-        build_y<HDP>(vv, lg, vy);
+        build_y<HDP, TERMS>(kv, lg, ky);
+        build_y<HDP, TERMS>(vv, lg, vy);
     }
     const uint16_t* qxg = a.qx + (int64_t)bh * a.nqt * G::XT;
     const uint16_t* gxg = a.gx + (int64_t)bh * a.nqt * G::XT;
@@ -728,14 +768,14 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
             for (int st = 0; st < 4; ++st) {
                 const float2 l01 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg);
                 const float2 l23 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg + 2);
-                s[st] = sprod<HDP>(qx, st, ky, (mf4){l01.x, l01.y, l23.x, l23.y}, ln, lg);   // S - lse2
+                s[st] = sprod<HDP, TERMS>(qx, st, ky, (mf4){l01.x, l01.y, l23.x, l23.y}, ln, lg);   // S - lse2
                 mf4 di = {0.f, 0.f, 0.f, 0.f};
                 if (!DROP) {
                     const float2 d01 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg);
                     const float2 d23 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg + 2);
                     di = (mf4){d01.x, d01.y, d23.x, d23.y};
                 }
-                dp[st] = sprod<HDP>(gx, st, vy, di, ln, lg);   // dP (- delta)
+                dp[st] = sprod<HDP, TERMS>(gx, st, vy, di, ln, lg);   // dP (- delta)
             }
             // lane: s[st][i] = S[query i0 + 16 st + 4 lg + i][key kj]
             const bool edge = (i0 + MT > a.Tq) || !kok || (a.causal > 0 && i0 < j0 + 16 - a.causal + 1);
@@ -766,20 +806,18 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
                     s[st][i] = p * g;   // dS
                 }
             }
-            dv = zprod<HDP>(gz, pd, dv, ln, lg);   // dV^T += dO^T Pd
-            dk = zprod<HDP>(qz, s, dk, ln, lg);    // dK^T += Q2^T dS
+            dv = zprod<HDP, TERMS>(gz, pd, dv, ln, lg);   // dV^T += dO^T Pd
+            dk = zprod<HDP, TERMS>(qz, s, dk, ln, lg);    // dK^T += Q2^T dS
         });
-    dk = zfinish<HDP>(dk);
-    dv = zfinish<HDP>(dv);
-    if (kok && zrow_owner<HDP>(lg)) {
-        float* krow = a.dk + rk;
-        float* vrow = a.dv + rv;
+    dk = zfinish<HDP, TERMS>(dk);
+    dv = zfinish<HDP, TERMS>(dv);
+    if (kok && zrow_owner<HDP, TERMS>(lg)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
             if (d < a.hd) {
-                krow[d] = dk[i] * kLn2;   // staged q2 = q * scale * log2e
-                vrow[d] = dv[i];
+                stf<T>(a.dk, rk + d, dk[i] * kLn2);   // staged q2 = q * scale * log2e
+                stf<T>(a.dv, rv + d, dv[i]);
             }
         }
     }
@@ -787,20 +825,20 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
 
 // the backward's two halves in one launch: z = 0 dq blocks (query tiles), z = 1 dk/dv blocks (key
 // tiles); dq's causal tail overlaps the first dk/dv blocks
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 __global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(MhaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lds[];
     if (blockIdx.z == 0) {
         if ((int)blockIdx.x >= a.nqt) return;
-        mha_dq_body<HDP, DROP>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x);
+        mha_dq_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x);
     } else {
         if ((int)blockIdx.x >= a.nkt) return;
-        mha_dkv_body<HDP, DROP>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nkt) : (int)blockIdx.x);
+        mha_dkv_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nkt) : (int)blockIdx.x);
     }
 }
 
 // head-averaged (dropped) probabilities: probs[b, i, j] = mean_h keep * softmax_j(...) / (1 - p)
-template <bool DROP>
+template <bool DROP, typename T>
 __global__ __launch_bounds__(256) void mha_probs_kernel(MhaArgs a) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over (b, i, j)
     if (e >= (int64_t)a.B * a.Tq * a.Tk) return;
@@ -811,10 +849,10 @@ __global__ __launch_bounds__(256) void mha_probs_kernel(MhaArgs a) {
     const bool vis = a.causal <= 0 || j - i < a.causal;
     if (vis) {
         for (int h = 0; h < a.H; ++h) {
-            const float* q = a.q + ((int64_t)i * a.B + b) * a.qs + h * a.hd;
-            const float* k = a.k + ((int64_t)j * a.B + b) * a.ks + h * a.hd;
+            const int64_t qo = ((int64_t)i * a.B + b) * a.qs + h * a.hd;
+            const int64_t ko = ((int64_t)j * a.B + b) * a.ks + h * a.hd;
             float s = 0.f;
-            for (int c = 0; c < a.hd; ++c) s = fmaf(q[c], k[c], s);
+            for (int c = 0; c < a.hd; ++c) s = fmaf(ldf<T>(a.q, qo + c), ldf<T>(a.k, ko + c), s);
             float p = fast_exp2(s * a.scale2 - a.lse[((int64_t)b * a.H + h) * a.Tq + i] * kLog2e);
             if (DROP) p = drop_keep(drop_row(a.seed, b * a.H + h, a.Tq, i), j, a.thresh) ? p * a.inv_keep : 0.f;
             sum += p;
@@ -846,6 +884,7 @@ static int mha_fill(const mmni_mha_desc* d, MhaArgs& a) {
     MMNI_ARG_CHECK((int64_t)d->B * d->heads <= 65535, "mha: B*heads exceeds the grid y limit");
     MMNI_ARG_CHECK((int64_t)d->B * d->heads * d->Tq < (1ll << 31), "mha: too many rows");
     MMNI_ARG_CHECK(d->dropout >= 0.f && d->dropout < 1.f, "mha: dropout must be in [0, 1)");
+    MMNI_ARG_CHECK(d->dtype == 0 || d->dtype == 1, "mha: dtype must be 0 (fp32) or 1 (bf16)");
     a.Tq = d->Tq; a.Tk = d->Tk; a.B = d->B; a.H = d->heads; a.hd = d->head_dim; a.causal = d->causal_diag;
     a.scale = d->scale;
     a.scale2 = d->scale * kLog2e;
@@ -855,6 +894,7 @@ static int mha_fill(const mmni_mha_desc* d, MhaArgs& a) {
     const double t = keep * 4294967296.0;
     a.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
     a.seed = d->seed;
+    a.bf16 = d->dtype == 1;
     a.nqt = (a.Tq + MT - 1) / MT;
     a.nkt = (a.Tk + MT - 1) / MT;
     return 0;
@@ -868,8 +908,9 @@ struct MhaWs {
     size_t delta, kx, kz, vx, vz, qx, qz, gx, gz, total;
 };
 static MhaWs mha_ws_layout(const MhaArgs& a, bool bwd) {
-    const int HDP = hd_pad(a.hd);
-    const int NX = (3 * HDP + 31) / 32, EW = 32 * NX, ZR = HDP <= 8 ? 16 : 32, ZW = HDP <= 8 ? 128 : 64;
+    const int HDP = hd_pad(a.hd), TERMS = a.bf16 ? 1 : 3;
+    const bool RS = TERMS == 3 && HDP <= 8;
+    const int NX = (TERMS * HDP + 31) / 32, EW = 32 * NX, ZR = TERMS == 1 ? 16 : (RS ? 16 : 32), ZW = RS ? 128 : 64;
     const size_t bhn = (size_t)a.B * a.H, xt = (size_t)MT * EW * 2, zt = (size_t)ZR * ZW * 2;
     const size_t nk = bhn * ((a.Tk + MT - 1) / MT), nq = bhn * ((a.Tq + MT - 1) / MT);
     MhaWs w{};
@@ -896,7 +937,7 @@ static MhaWs mha_ws_layout(const MhaArgs& a, bool bwd) {
     return w;
 }
 
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 static int mha_fwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     const MhaWs w = mha_ws_layout(a, false);
     uint16_t* kx = reinterpret_cast<uint16_t*>(ws + w.kx);
@@ -906,17 +947,17 @@ static int mha_fwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     sa.op[0] = SplitOp{a.k, a.ks, a.Tk, a.nkt, 1.f, -1, kx, nullptr};
     sa.op[1] = SplitOp{a.v, a.vs, a.Tk, a.nkt, 1.f, (!DROP && a.hd < HDP) ? a.hd : -1, nullptr, vz};
     sa.nops = 2;
-    mha_split_kernel<HDP><<<dim3(a.nkt, a.B * a.H), 256, 0, s>>>(sa);
+    mha_split_kernel<HDP, T><<<dim3(a.nkt, a.B * a.H), 256, 0, s>>>(sa);
     int rc = launch_status("mha_split");
     if (rc) return rc;
     a.kx = kx;
     a.vz = vz;
     dim3 grid(a.nqt, a.B * a.H);
-    mha_fwd_mfma_kernel<HDP, DROP><<<grid, 256, 0, s>>>(a);
+    mha_fwd_mfma_kernel<HDP, DROP, T><<<grid, 256, 0, s>>>(a);
     return launch_status("mha_fwd");
 }
 
-template <int HDP, bool DROP>
+template <int HDP, bool DROP, typename T>
 static int mha_bwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     const MhaWs w = mha_ws_layout(a, true);
     a.delta = reinterpret_cast<float*>(ws + w.delta);
@@ -929,25 +970,33 @@ static int mha_bwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     sa.op[3] = SplitOp{a.dout, a.os, a.Tq, a.nqt, 1.f, -1, img(w.gx), img(w.gz)};
     sa.nops = 4;
     sa.o = a.o; sa.g = a.dout; sa.os = a.os; sa.Tq = a.Tq; sa.delta = a.delta;
-    mha_split_kernel<HDP><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H), 256, 0, s>>>(sa);
+    mha_split_kernel<HDP, T><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H), 256, 0, s>>>(sa);
     int rc = launch_status("mha_split");
     if (rc) return rc;
     a.kx = img(w.kx); a.kz = img(w.kz); a.vx = img(w.vx);
     a.qx = img(w.qx); a.qz = img(w.qz); a.gx = img(w.gx); a.gz = img(w.gz);
-    const int lds = DqLds<HDP>::BYTES > DkvLds<HDP>::BYTES ? DqLds<HDP>::BYTES : DkvLds<HDP>::BYTES;
-    mha_bwd_mfma_kernel<HDP, DROP><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H, 2), 256, lds, s>>>(a);
+    constexpr int TERMS = kTerms<T>;
+    const int lds = DqLds<HDP, TERMS>::BYTES > DkvLds<HDP, TERMS>::BYTES ? DqLds<HDP, TERMS>::BYTES
+                                                                         : DkvLds<HDP, TERMS>::BYTES;
+    mha_bwd_mfma_kernel<HDP, DROP, T><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H, 2), 256, lds, s>>>(a);
     return launch_status("mha_bwd");
 }
 
+#define MMNI_MHA_DISPATCH_T(FN, T)                                                        \
+    switch (hd_pad(a.hd)) {                                                               \
+        case 4: return drop ? FN<4, true, T>(a, ws_, st_) : FN<4, false, T>(a, ws_, st_);   \
+        case 8: return drop ? FN<8, true, T>(a, ws_, st_) : FN<8, false, T>(a, ws_, st_);   \
+        default: return drop ? FN<16, true, T>(a, ws_, st_) : FN<16, false, T>(a, ws_, st_); \
+    }
 #define MMNI_MHA_DISPATCH(FN)                                                             \
     {                                                                                     \
         const bool drop = a.thresh != 0xffffffffu;                                        \
         hipStream_t st_ = (hipStream_t)stream;                                            \
         char* ws_ = static_cast<char*>(workspace);                                        \
-        switch (hd_pad(a.hd)) {                                                           \
-            case 4: return drop ? FN<4, true>(a, ws_, st_) : FN<4, false>(a, ws_, st_);   \
-            case 8: return drop ? FN<8, true>(a, ws_, st_) : FN<8, false>(a, ws_, st_);   \
-            default: return drop ? FN<16, true>(a, ws_, st_) : FN<16, false>(a, ws_, st_); \
+        if (a.bf16) {                                                                     \
+            MMNI_MHA_DISPATCH_T(FN, __bf16)                                               \
+        } else {                                                                          \
+            MMNI_MHA_DISPATCH_T(FN, float)                                                \
         }                                                                                 \
     }
 
@@ -967,8 +1016,8 @@ extern "C" size_t mmni_mha_bwd_workspace_bytes(const mmni_mha_desc* d) {
     return mha_ws_layout(a, true).total;
 }
 
-extern "C" int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                            float* out, float* lse, void* workspace, void* stream) {
+extern "C" int mmni_mha_fwd(const mmni_mha_desc* d, const void* q, const void* k, const void* v,
+                            void* out, float* lse, void* workspace, void* stream) {
     MhaArgs a{};
     int rc = mha_fill(d, a);
     if (rc) return rc;
@@ -978,9 +1027,9 @@ extern "C" int mmni_mha_fwd(const mmni_mha_desc* d, const float* q, const float*
     MMNI_MHA_DISPATCH(mha_fwd_launch)
 }
 
-extern "C" int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float* k, const float* v,
-                            const float* out, const float* dout, const float* lse, float* dq, float* dk,
-                            float* dv, void* workspace, void* stream) {
+extern "C" int mmni_mha_bwd(const mmni_mha_desc* d, const void* q, const void* k, const void* v,
+                            const void* out, const void* dout, const float* lse, void* dq, void* dk,
+                            void* dv, void* workspace, void* stream) {
     MhaArgs a{};
     int rc = mha_fill(d, a);
     if (rc) return rc;
@@ -991,7 +1040,7 @@ extern "C" int mmni_mha_bwd(const mmni_mha_desc* d, const float* q, const float*
     MMNI_MHA_DISPATCH(mha_bwd_launch)
 }
 
-extern "C" int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const float* k, const float* lse,
+extern "C" int mmni_mha_mean_probs(const mmni_mha_desc* d, const void* q, const void* k, const float* lse,
                                    float* probs, void* stream) {
     MhaArgs a{};
     int rc = mha_fill(d, a);
@@ -1000,9 +1049,11 @@ extern "C" int mmni_mha_mean_probs(const mmni_mha_desc* d, const float* q, const
     a.q = q; a.k = k; a.lse = const_cast<float*>(lse); a.probs = probs;
     const int64_t n = (int64_t)a.B * a.Tq * a.Tk;
     if (a.thresh != 0xffffffffu)
-        mha_probs_kernel<true><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a);
+        a.bf16 ? mha_probs_kernel<true, __bf16><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a)
+               : mha_probs_kernel<true, float><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a);
     else
-        mha_probs_kernel<false><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a);
+        a.bf16 ? mha_probs_kernel<false, __bf16><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a)
+               : mha_probs_kernel<false, float><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(a);
     return launch_status("mha_probs");
 }
 

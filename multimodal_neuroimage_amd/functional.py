@@ -243,8 +243,10 @@ def _workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 256), device=device, dtype=torch.uint8)
 
 
-def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_, dropout=0.0, seed=0):
+def _mha_desc(Tq, Tk, B, heads, hd, causal_diag, scale, qs, ks, vs, os_, dropout=0.0, seed=0,
+              dtype=torch.float32):
     d = _lib.MhaDesc()
+    d.dtype = 1 if dtype == torch.bfloat16 else 0
     d.Tq, d.Tk, d.B, d.heads, d.head_dim = Tq, Tk, B, heads, hd
     d.causal_diag = int(causal_diag)
     d.scale = float(scale)
@@ -263,23 +265,26 @@ def dropout_seed():
 class _MHA(torch.autograd.Function):
     """q (Tq, B, E), k/v (Tk, B, E) dense time-major tensors -> out (Tq, B, E), lse (B, h, Tq).
     dropout p > 0 applies the counter-based mask of `seed` to the probabilities (the backward
-    regenerates it)."""
+    regenerates it).  fp32 or bf16 storage (all three alike; out and the gradients follow it)."""
 
     @staticmethod
     def forward(ctx, q, k, v, heads, causal_diag, scale, dropout, seed):
-        require_device(q, k, v, what="mha")
+        require_device(q, k, v, what="mha", dtypes=(torch.float32, torch.bfloat16))
+        if not (q.dtype == k.dtype == v.dtype):
+            raise RuntimeError(f"mha: q/k/v dtypes differ ({q.dtype}, {k.dtype}, {v.dtype})")
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         Tq, B, E = q.shape
         Tk = k.shape[0]
-        out = torch.empty((Tq, B, E), device=q.device, dtype=torch.float32)
+        out = torch.empty((Tq, B, E), device=q.device, dtype=q.dtype)
         lse = torch.empty((B, heads, Tq), device=q.device, dtype=torch.float32)
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed, q.dtype)
         lib = _lib.load()
         ws = _workspace(lib.mmni_mha_fwd_workspace_bytes(d), q.device)
         ev = KernelTimer.start()
         check(lib.mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse), ptr(ws),
                                stream_handle(q.device)), "mmni_mha_fwd")
-        KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
+        sfx = "_bf16" if q.dtype == torch.bfloat16 else ""
+        KernelTimer.stop(f"mha_fwd_E{E}{sfx}", ev, 4.0 * Tq * Tk * B * E, q.element_size() * B * E * (2 * Tq + 2 * Tk))
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.cfg = (heads, causal_diag, scale, dropout, seed)
         ctx.mark_non_differentiable(lse)
@@ -291,18 +296,19 @@ class _MHA(torch.autograd.Function):
         heads, causal_diag, scale, dropout, seed = ctx.cfg
         Tq, B, E = q.shape
         Tk = k.shape[0]
-        dout = dout.contiguous()
+        dout = dout.contiguous().to(q.dtype)
         dq = torch.empty_like(q)
         dk = torch.empty_like(k)
         dv = torch.empty_like(v)
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed, q.dtype)
         lib = _lib.load()
         ws = _workspace(lib.mmni_mha_bwd_workspace_bytes(d), q.device)
         ev = KernelTimer.start()
         check(lib.mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse),
                                ptr(dq), ptr(dk), ptr(dv), ptr(ws), stream_handle(q.device)),
               "mmni_mha_bwd")
-        KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
+        sfx = "_bf16" if q.dtype == torch.bfloat16 else ""
+        KernelTimer.stop(f"mha_bwd_E{E}{sfx}", ev, 10.0 * Tq * Tk * B * E, q.element_size() * B * E * (4 * Tq + 4 * Tk))
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -332,7 +338,7 @@ def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None, dropout=0.0, see
     if k.stride(1) != E or k.stride(0) != B * E:
         k = k.contiguous()
     probs = torch.empty((B, Tq, Tk), device=q.device, dtype=torch.float32)
-    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed)
+    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed, q.dtype)
     check(_lib.load().mmni_mha_mean_probs(d, ptr(q), ptr(k), ptr(lse), ptr(probs), stream_handle(q.device)),
           "mmni_mha_mean_probs")
     return probs

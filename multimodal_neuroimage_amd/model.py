@@ -522,6 +522,12 @@ class SwinCrossmodal3D(BaseModel):
                        out_layer1/2; nlevels layers, num_heads_mult heads, causal mask) on the
                        L = (volume / patch)^3 token sequences, feature_map_gen 'no'.
     forward(A, B): two (B, D, H, W) volumes -> {'embedding_per_ROIs', fine_tune_task: (B, 1)}.
+
+    C5: modality B may have its own volume and patch (`volume_size_B`,
+    `patch_size_B`; 128^3 fMRI / 8 and 96^3 sMRI / 6 both give 16^3 tokens), and
+    `head_dtype='bf16'` runs to_seq + the crossmodal head under bf16 autocast: fp32 master
+    weights, bf16 GEMMs and activations, the bf16 MHA kernels on bf16 q/k/v, fp32 LayerNorm and
+    softmax.  The Swin front-end (<1% of C5's FLOPs) stays fp32.
     """
 
     def __init__(self, **kwargs):
@@ -538,13 +544,22 @@ class SwinCrossmodal3D(BaseModel):
         d = kwargs.get('intermediate_vec') or 84
         use_ckpt = bool(kwargs.get('use_checkpoint', False))
         V, P, E = self.volume_size, self.patch_size, self.embed_dim
+        VB = kwargs.get('volume_size_B') or V
+        PB = kwargs.get('patch_size_B') or P
+        hd = kwargs.get('head_dtype') or 'fp32'
+        if hd not in ('fp32', 'bf16'):
+            raise ValueError(f"head_dtype must be 'fp32' or 'bf16', got {hd!r}")
+        self.head_dtype = torch.bfloat16 if hd == 'bf16' else torch.float32
 
-        def embed():
-            return PatchEmbed(img_size_w=V, img_size_h=V, patch_size=P, in_chans=1, embed_dim=E,
-                              norm_layer=nn.LayerNorm, img_size_d=V)
+        def embed(v, p):
+            return PatchEmbed(img_size_w=v, img_size_h=v, patch_size=p, in_chans=1, embed_dim=E,
+                              norm_layer=nn.LayerNorm, img_size_d=v)
 
-        self.patch_embed_A, self.patch_embed_B = embed(), embed()
+        self.patch_embed_A, self.patch_embed_B = embed(V, P), embed(VB, PB)
         res = tuple(self.patch_embed_A.patches_resolution)
+        if tuple(self.patch_embed_B.patches_resolution) != res:
+            raise ValueError(f"modality token grids differ: {res} vs {tuple(self.patch_embed_B.patches_resolution)} "
+                             "(volume_size / patch_size must match volume_size_B / patch_size_B)")
         self.patches_resolution = res
 
         def stage():
@@ -568,4 +583,8 @@ class SwinCrossmodal3D(BaseModel):
         x = self.swin_A(self.patch_embed_A(A.unsqueeze(1)))
         y = self.swin_B(self.patch_embed_B(B.unsqueeze(1)))
         x, y = self.cross(x, y, self.patches_resolution)
-        return self.crossmodal(self.to_seq_A(x), self.to_seq_B(y))
+        if self.head_dtype == torch.float32:
+            return self.crossmodal(self.to_seq_A(x), self.to_seq_B(y))
+        with torch.autocast(device_type="cuda", dtype=self.head_dtype):
+            out = self.crossmodal(self.to_seq_A(x), self.to_seq_B(y))
+        return {k: (v.float() if torch.is_tensor(v) else v) for k, v in out.items()}

@@ -284,11 +284,13 @@ def crossmodal_head(p, pre, x_l, x_u, layers, heads, feature_map_gen="no", attn_
 def swin_crossmodal_logits(p, A, Bv, cfg):
     """SwinCrossmodal3D (SURVEY §8d C4 composite): per modality Conv3d(k=s=patch) + LN + Swin-V2
     stage 1, Cross_BasicLayer, Linear to d, crossmodal head.  cfg: patch, window_size, swin_heads,
-    cross_heads, depth, layers, heads."""
-    ws, P = cfg["window_size"], cfg["patch"]
+    cross_heads, depth, layers, heads [, patch_B: modality B's patch (C5), default patch]."""
+    ws = cfg["window_size"]
+    patches = {"A": cfg["patch"], "B": cfg.get("patch_B", cfg["patch"])}
 
     def stage(img, tag):
         B = img.shape[0]
+        P = patches[tag]
         t = O.conv3d_cl(img.unsqueeze(-1), p[f"patch_embed_{tag}.proj.weight"], p[f"patch_embed_{tag}.proj.bias"],
                         (P,) * 3, 0)
         res = tuple(t.shape[1:-1])

@@ -13,11 +13,12 @@ from multimodal_neuroimage_amd import functional as MF  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 dev = torch.device("cuda:0")
 res = {}
-for T, E in [(1728, 84), (1728, 168), (4096, 84)]:
+for T, E, dt in [(1728, 84, torch.float32), (1728, 168, torch.float32), (4096, 84, torch.float32),
+                 (4096, 84, torch.bfloat16), (4096, 168, torch.bfloat16), (1728, 84, torch.bfloat16)]:
     B, heads = 4, 12
     g = torch.Generator(device=dev).manual_seed(T + E)
-    q, k, v = [torch.randn(T, B, E, device=dev, generator=g, requires_grad=True) for _ in range(3)]
-    go = torch.randn(T, B, E, device=dev, generator=g)
+    q, k, v = [torch.randn(T, B, E, device=dev, generator=g).to(dt).requires_grad_(True) for _ in range(3)]
+    go = torch.randn(T, B, E, device=dev, generator=g).to(dt)
     diag = 1
     for _ in range(2):
         out, lse = MF.mha_core(q, k, v, heads, diag)

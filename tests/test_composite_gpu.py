@@ -49,3 +49,69 @@ def test_swin_crossmodal3d_vs_oracle(device):
     for k in ("patch_embed_A.proj.weight", "swin_B.blocks.1.attn.logit_scale", "cross.blocks.1.attn_A.q.weight",
               "to_seq_B.weight", "crossmodal.trans_mem.layers.1.fc1.weight", "crossmodal.out_layer2.weight"):
         assert rel(named[k].grad, p[k].grad) < 2e-3, k
+
+
+def _torch_bf16_core(q, k, v, heads, diag, scale, dropout=0.0, seed=0):
+    """The reference's attention core in torch (multihead_attention.py:109-125: bmm, fp32 softmax,
+    type_as, bmm) -- the yardstick for what bf16 storage itself costs in gradient accuracy."""
+    Tq, B, E = q.shape
+    Tk = k.shape[0]
+    d = E // heads
+    qh = (q * scale).reshape(Tq, B * heads, d).transpose(0, 1)
+    kh = k.reshape(Tk, B * heads, d).transpose(0, 1)
+    vh = v.reshape(Tk, B * heads, d).transpose(0, 1)
+    w = torch.bmm(qh, kh.transpose(1, 2))
+    if diag > 0:
+        w = w + torch.triu(torch.full((Tq, Tk), float("-inf"), device=q.device), diag).to(w.dtype)
+    w = torch.softmax(w.float(), dim=-1).type_as(w)
+    return torch.bmm(w, vh).transpose(0, 1).reshape(Tq, B, E), torch.zeros(B, heads, Tq, device=q.device)
+
+
+def test_swin_crossmodal3d_c5_bf16_head_vs_oracle(device, monkeypatch):
+    """The C5 family at reduced size: fMRI 64^3 / patch 8 and sMRI 48^3 / patch 6
+    (8^3 tokens each), window 4, crossmodal head under bf16 autocast (bf16 GEMMs and the bf16 MHA
+    kernels), against the fp64 oracle.  Logits and input gradients: 2e-2 max-rel (the C5
+    tolerance).  The head's parameter gradients are sums of bf16-rounded products with heavy
+    cancellation and deviate by several percent under ANY bf16 autocast; they are held to the
+    error of the same model whose attention core is the reference's torch code in bf16."""
+    from multimodal_neuroimage_amd.modules import multihead_attention as MHA_MOD
+    kw = c4_kwargs(volume=64, layers=2)
+    kw.update(volume_size_B=48, patch_size_B=6, window_size=4, head_dtype="bf16")
+    A = torch.from_numpy(recipe.randn(5100, (2, 64, 64, 64)))
+    Bv = torch.from_numpy(recipe.randn(5101, (2, 48, 48, 48)))
+    tgt = torch.tensor([[1.0], [0.0]])
+    errs = {}
+    for mode in ("kernels", "torch"):
+        if mode == "torch":
+            monkeypatch.setattr(MHA_MOD, "mha_core", _torch_bf16_core)
+        m = M.SwinCrossmodal3D(**kw)
+        recipe.fill_params(m)
+        if mode == "kernels":
+            p = OM.params_of(m)
+            A64, B64 = A.double().requires_grad_(True), Bv.double().requires_grad_(True)
+            cfg = dict(patch=8, patch_B=6, window_size=4, swin_heads=3, cross_heads=6, depth=2, layers=2, heads=12)
+            ref = OM.swin_crossmodal_logits(p, A64, B64, cfg)
+            torch.nn.functional.binary_cross_entropy_with_logits(ref, tgt.double()).backward()
+        m = m.to(device)
+        Ad, Bd = A.to(device).requires_grad_(True), Bv.to(device).requires_grad_(True)
+        out = m(Ad, Bd)["binary_classification"]
+        assert out.dtype == torch.float32
+        torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device)).backward()
+        torch.cuda.synchronize()
+        if mode == "kernels":
+            assert rel(out, ref) < 2e-2
+            assert rel(Ad.grad, A64.grad) < 2e-2
+            assert rel(Bd.grad, B64.grad) < 2e-2
+            named = dict(m.named_parameters())
+            for k in ("patch_embed_A.proj.weight", "patch_embed_B.proj.weight", "cross.blocks.1.attn_A.q.weight"):
+                assert named[k].grad.dtype == torch.float32, k
+                assert rel(named[k].grad, p[k].grad) < 2e-2, k
+        for k, prm in m.named_parameters():
+            if k.startswith(("crossmodal.", "to_seq")) and prm.grad is not None and p[k].grad is not None:
+                a, b = prm.grad.double().cpu(), p[k].grad
+                errs.setdefault(k, {})[mode] = float((a - b).norm() / max(float(b.norm()), 1e-30))
+    ours = np.array([v["kernels"] for v in errs.values()])
+    theirs = np.array([v["torch"] for v in errs.values()])
+    assert float(np.median(ours)) <= 1.1 * float(np.median(theirs)) + 1e-3, (np.median(ours), np.median(theirs))
+    for k, v in errs.items():
+        assert v["kernels"] <= 1.5 * v["torch"] + 5e-3, (k, v)

@@ -168,6 +168,43 @@ def test_mha_fwd_bwd_vs_oracle(device, Tq, Tk, B, heads, hd, causal):
         assert rel_err(a.grad, b.grad) < TOL
 
 
+MHA_BF16 = [
+    # Tq, Tk, B, heads, hd, causal  (C5: bf16 storage, one bf16 product, fp32 accumulation)
+    (368, 368, 2, 12, 7, True),
+    (200, 200, 2, 12, 14, True),
+    (50, 70, 2, 12, 14, True),
+    (64, 96, 1, 4, 8, False),
+    (130, 130, 1, 6, 4, True),
+    (1024, 1024, 1, 12, 7, True),
+]
+TOL_BF16 = 2e-2   # bf16 runs are held to 2e-2 rel against the fp32/fp64 golden
+
+
+@pytest.mark.parametrize("Tq,Tk,B,heads,hd,causal", MHA_BF16)
+def test_mha_bf16_vs_oracle(device, Tq, Tk, B, heads, hd, causal):
+    """bf16 q/k/v/dout in, bf16 out/dq/dk/dv: against the fp64 oracle on the same bf16-rounded
+    inputs, 2e-2 max-rel; the head-averaged weights (fp32) too."""
+    gen = torch.Generator().manual_seed(Tq * 1000 + Tk + hd + 7)
+    E = heads * hd
+    q, k, v = [torch.randn(T, B, E, generator=gen, dtype=torch.float64).bfloat16().double() for T in (Tq, Tk, Tk)]
+    gout = torch.randn(Tq, B, E, generator=gen, dtype=torch.float64).bfloat16().double()
+    diag = O.causal_diag(Tq, Tk) if causal else 0
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    ref, ref_w = O.mha_core(*leaves, heads, diag)
+    (ref * gout).sum().backward()
+    dev = [t.bfloat16().to(device).requires_grad_(True) for t in (q, k, v)]
+    out, lse = MF.mha_core(*dev, heads, diag)
+    assert out.dtype == torch.bfloat16
+    out.backward(gout.bfloat16().to(device))
+    w = MF.mha_mean_probs(dev[0], dev[1], lse, heads, diag)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL_BF16
+    assert rel_err(w, ref_w) < TOL_BF16
+    for a, b in zip(dev, leaves):
+        assert a.grad.dtype == torch.bfloat16
+        assert rel_err(a.grad, b.grad) < TOL_BF16
+
+
 CONV = [
     # B, (D,H,W), Cin, Cout, k, stride, pad, slope
     (2, (16, 16, 16), 1, 12, (8, 8, 8), (8, 8, 8), (0, 0, 0), 1.0),
