@@ -837,3 +837,64 @@ def linear(x, lin_or_weight, bias=None, residual=None):
         y = F.linear(x, weight, bias)
         return y if residual is None else residual + y
     return _TokenLinear.apply(x, weight, bias, residual)
+
+
+# ------------------------------------------------------------------------------------------
+# split-K weight gradient for the crossmodal encoder's Linears
+# ------------------------------------------------------------------------------------------
+def _splitk_chunks(rows):
+    """Row chunks of a split-K weight gradient: the largest S <= 64 dividing `rows` with >= 256 rows
+    per chunk (1: no split)."""
+    best = 1
+    for S in range(2, 65):
+        if rows % S == 0 and rows // S >= 256:
+            best = S
+    return best
+
+
+class _SplitKLinear(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient contracts over the token rows in S chunks (one batched
+    GEMM of S small products, then a fixed-order fp32 sum over S; deterministic).  dW = dY^T X has a
+    tiny N x K output and K = T*B = 6,912 (C4) to 32,768 (C5) rows, where the library's single
+    GEMM tiles only the output and runs a few dozen workgroups (57-114 us a call, profiles/).
+    Under bf16 autocast the products run in bf16 like F.linear's; the gradients come back in the
+    parameters' own dtype."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        cdt = dy.dtype
+        N, K = w.shape
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy @ w.to(cdt)).to(x.dtype)
+        dy2 = dy.reshape(-1, N)
+        x2 = x.reshape(-1, K).to(cdt)
+        rows = dy2.shape[0]
+        acc = torch.promote_types(cdt, torch.float32)   # fp32 sums (fp64 stays fp64)
+        S = _splitk_chunks(rows)
+        if S > 1:
+            r = rows // S
+            dw = torch.bmm(dy2.view(S, r, N).transpose(1, 2), x2.view(S, r, K)).to(acc).sum(0)
+        else:
+            dw = (dy2.t() @ x2).to(acc)
+        db = dy2.to(acc).sum(0).to(w.dtype) if ctx.has_bias else None
+        return dx, dw.to(w.dtype), db
+
+
+def splitk_linear(x, weight, bias=None):
+    """F.linear with the split-K weight gradient (see _SplitKLinear)."""
+    return _SplitKLinear.apply(x, weight, bias)
+
+
+class SplitKLinear(torch.nn.Linear):
+    """nn.Linear (same parameters and state_dict keys) with the split-K weight gradient."""
+
+    def forward(self, x):
+        return _SplitKLinear.apply(x, self.weight, self.bias)

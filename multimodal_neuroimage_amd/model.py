@@ -25,7 +25,7 @@ from .modules.swin_v2_module import BasicLayer, PatchEmbed, PatchMerging
 from .modules.swinfusion_module import (RSTB, CRSTB, PatchEmbed_fusion, PatchUnEmbed, Upsample, UpsampleOneStep,
                                         Cross_BasicLayer, conv_tokens)
 from .modules._common import trunc_normal_
-from .functional import layer_norm
+from .functional import SplitKLinear, layer_norm
 
 
 class BaseModel(nn.Module, ABC):
@@ -570,8 +570,8 @@ class SwinCrossmodal3D(BaseModel):
         self.swin_A, self.swin_B = stage(), stage()
         self.cross = Cross_BasicLayer(dim=E, input_resolution=res, depth=depth, num_heads=cross_heads, window_size=ws,
                                       mlp_ratio=mlp_ratio, use_checkpoint=use_ckpt)
-        self.to_seq_A = nn.Linear(E, d)
-        self.to_seq_B = nn.Linear(E, d)
+        self.to_seq_A = SplitKLinear(E, d)
+        self.to_seq_B = SplitKLinear(E, d)
         head_kw = dict(kwargs)
         head_kw.update(intermediate_vec=d, feature_map_gen='no', feature_map_size='same',
                        sequence_length=int(res[0] * res[1] * res[2]))

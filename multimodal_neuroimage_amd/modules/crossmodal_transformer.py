@@ -12,6 +12,7 @@ import torch.nn.functional as F
 
 from .position_embedding import SinusoidalPositionalEmbedding
 from .multihead_attention import MultiheadAttention
+from ..functional import SplitKLinear
 
 
 class TransformerEncoder(nn.Module):
@@ -140,7 +141,9 @@ class _CausalMask:
 
 
 def Linear(in_features, out_features, bias=True):
-    m = nn.Linear(in_features, out_features, bias)
+    """nn.Linear (crossmodal_transformer.py:189-194) whose weight gradient is split over the token
+    rows (functional.SplitKLinear; same parameters and state_dict keys)."""
+    m = SplitKLinear(in_features, out_features, bias)
     nn.init.xavier_uniform_(m.weight)
     if bias:
         nn.init.constant_(m.bias, 0.)

@@ -17,7 +17,7 @@ from torch import nn
 from torch.nn import Parameter
 import torch.nn.functional as F
 
-from ..functional import dropout_seed, mha_core, mha_mean_probs
+from ..functional import SplitKLinear, dropout_seed, mha_core, mha_mean_probs, splitk_linear
 
 
 def causal_diag_of(attn_mask, Tq, Tk):
@@ -51,7 +51,7 @@ class MultiheadAttention(nn.Module):
         self.register_parameter('in_proj_bias', None)
         if bias:
             self.in_proj_bias = Parameter(torch.Tensor(3 * embed_dim))
-        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=bias)
+        self.out_proj = SplitKLinear(embed_dim, embed_dim, bias=bias)
         if add_bias_kv:
             self.bias_k = Parameter(torch.Tensor(1, 1, embed_dim))
             self.bias_v = Parameter(torch.Tensor(1, 1, embed_dim))
@@ -119,4 +119,4 @@ class MultiheadAttention(nn.Module):
         bias = kwargs.get('bias', self.in_proj_bias)
         if bias is not None:
             bias = bias[start:end]
-        return F.linear(input, weight, bias)
+        return splitk_linear(input, weight, bias)
