@@ -726,6 +726,10 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     MMNI_ARG_CHECK(row_aligned(q, d->q_stride, d->C) && row_aligned(k, d->k_stride, d->C) &&
                        row_aligned(v, d->v_stride, d->C) && row_aligned(out, d->o_stride, d->C),
                    "wattn_fwd: q/k/v/out must be 16-byte aligned with strides multiple of 4");
+    if (wattn_bc_supported(a.g, d->C, d->heads, d->kind)) {   // 6^3 kind 0 head pairs: row-broadcast kernel
+        a.q = q; a.k = k; a.v = v; a.table = table; a.tau = table; a.out = out; a.lse = lse; a.vmax = vmax;
+        return wattn_bc_forward(a, d->heads, (hipStream_t)stream);
+    }
     void *kf, *kb;
     int maxt;
     bool packed = false;

@@ -436,6 +436,186 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// forward: lane = query pair (t, t + H); keys (n, n + H) broadcast from LDS as in pass A.
+// Online softmax with a lazy reference: scores are taken relative to a per-row reference m
+// (initialised from the first key) and m is raised -- with the rescale of l and o -- only when a
+// score exceeds it by more than kLazy (wave-uniform test).  So p = exp2(s - m) <= 2^kLazy, no
+// overflow, and the common step costs one exp per score and no rescale.  No software prefetch
+// of the next key: the 105-VGPR loop runs 4 waves per SIMD (the LDS footprint allows 8 blocks
+// per CU), and the other waves hide the broadcast reads.
+// ------------------------------------------------------------------------------------
+constexpr float kLazy = 8.0f;
+
+template <int WD, int WH, int WW, bool MASKED>
+__device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[2], Row (&o)[2], int cq,
+                                         const int (&rq)[2], const bc::Regions& reg, const float* tab,
+                                         const float* kv_s) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int EB = 8;
+    const char* tb = reinterpret_cast<const char*>(tab);
+    const uint32_t lane_base = (uint32_t)((cq - Wn::DC) * EB);
+    const f2* kv2 = reinterpret_cast<const f2*>(kv_s);
+    f2 kk[2][2], vv[2][2], tbm, tb0, tbp;
+    auto fetch = [&](const f2* kvk, const char* pe, f2 (&k_)[2][2], f2 (&v_)[2][2], f2& m_, f2& z_, f2& p_) {
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                k_[v][c] = kvk[v * 4 + c];
+                v_[v][c] = kvk[v * 4 + 2 + c];
+            }
+        m_ = *reinterpret_cast<const f2*>(pe);
+        z_ = *reinterpret_cast<const f2*>(pe + Wn::DC * EB);
+        p_ = *reinterpret_cast<const f2*>(pe + 2 * Wn::DC * EB);
+    };
+    fetch(kv2, tb + lane_base, kk, vv, tbm, tb0, tbp);
+    {   // the reference: each row's exact maximum over the first key's two rows
+        int rk[2] = {0, 0};
+        if (MASKED) {
+            rk[0] = bc::region_code(reg, 0, 0, 0);
+            rk[1] = bc::region_code(reg, WD / 2, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f2 sv[2];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                f2 base = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
+                if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                sv[v] = bc::pfma(q[u].x[1], kk[v][1], s);
+            }
+            m[u] = (f2){fmaxf(sv[0].x, sv[1].x), fmaxf(sv[0].y, sv[1].y)};
+        }
+    }
+    for (int i = 0; i < WD / 2; ++i) {
+        for (int j = 0; j < WH; ++j) {
+            const int code0 = i * Wn::TW + j * Wn::TH;
+            const f2* kvr = kv2 + (i * WH + j) * WW * 8;
+            const char* trow = tb + (lane_base - (uint32_t)((code0 + WW - 1) * EB));
+#pragma unroll
+            for (int k = 0; k < WW; ++k) {
+                fetch(kvr + k * 8, trow + (WW - 1 - k) * EB, kk, vv, tbm, tb0, tbp);
+                int rk[2] = {0, 0};
+                if (MASKED) {
+                    rk[0] = bc::region_code(reg, i, j, k);
+                    rk[1] = bc::region_code(reg, i + WD / 2, j, k);
+                }
+                f2 s[2][2];
+                float smax = -INFINITY;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
+                        f2 base = t - m[u];
+                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                        f2 sv = bc::pfma(q[u].x[0], kk[v][0], base);
+                        sv = bc::pfma(q[u].x[1], kk[v][1], sv);
+                        s[u][v] = sv;
+                        smax = fmaxf(smax, fmaxf(sv.x, sv.y));
+                    }
+                }
+                if (__any(smax > kLazy)) {   // rare: raise the reference of the rows that need it
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const f2 up = (f2){fmaxf(fmaxf(s[u][0].x, s[u][1].x), 0.f),
+                                           fmaxf(fmaxf(s[u][0].y, s[u][1].y), 0.f)};
+                        const f2 alpha = bc::exp2_2(-up);
+                        l[u] *= alpha;
+                        o[u].x[0] *= alpha;
+                        o[u].x[1] *= alpha;
+                        m[u] += up;
+                        s[u][0] -= up;
+                        s[u][1] -= up;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        const f2 p = bc::exp2_2(s[u][v]);
+                        l[u] += p;
+                        o[u].x[0] = bc::pfma(p, vv[v][0], o[u].x[0]);
+                        o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int WD, int WH, int WW>
+__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void wattn_fwd_bc_kernel(WAArgs a) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int H = Wn::H, TSZ = Wn::TSZ;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    float* tab_s = smem;                 // [TSZ] f2: bias * log2e of the head pair
+    float* kv_s = tab_s + TSZ * 2;       // [H][8] f2: key records as in pass A
+    const bc::Items it = bc::items(NHG);
+    const int tid = threadIdx.x;
+    const bool lane_ok = tid < H;
+    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab_s[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
+    const int coff = it.hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    float vabs = 0.f;
+    for (int w = it.first; w < g.nwin; w += it.stride) {
+        __syncthreads();   // previous window's K/V reads done (and the table staged, first time)
+        Row q[2], o[2];
+        f2 m[2], l[2];
+        int cq = 0, rq[2] = {0, 0};
+        int64_t row[2] = {0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int tt = t + u * H;
+                const TokenInfo ti = token_info(g, w, tt);
+                row[u] = ti.row;
+                rq[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
+                if (u == 0) cq = ti.code + Wn::OFF;
+                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
+                f2* kv2 = reinterpret_cast<f2*>(kv_s) + t * 8 + u * 4;   // key record t
+                kv2[0] = (f2){kr.x, kr.z};
+                kv2[1] = (f2){kr.y, kr.w};
+                kv2[2] = (f2){vr.x, vr.z};
+                kv2[3] = (f2){vr.y, vr.w};
+                l[u] = bc::splat(0.f);
+                o[u].x[0] = o[u].x[1] = bc::splat(0.f);
+            }
+        }
+        __syncthreads();
+        if (lane_ok) {
+            if (reg.masked) fwd_loop<WD, WH, WW, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+            else fwd_loop<WD, WH, WW, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
+                Row r;
+                r.x[0] = o[u].x[0] * inv;
+                r.x[1] = o[u].x[1] * inv;
+                bc::store_row_nat(a.out + row[u] * a.os + coff, r, 1.0f);
+                a.lse[row[u] * NHT + 2 * it.hp] = (m[u].x + fast_log2(l[u].x)) * kLn2;
+                a.lse[row[u] * NHT + 2 * it.hp + 1] = (m[u].y + fast_log2(l[u].y)) * kLn2;
+            }
+        }
+    }
+    if (a.vmax != nullptr) {
+        for (int off = 32; off > 0; off >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, off));
+        if ((tid & 63) == 0) atomicMax(a.vmax, __float_as_uint(vabs));
+    }
+}
+
 __global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < n) dtable[e] += src[e];
@@ -478,6 +658,22 @@ static int set_lds_limit(const void* fn, size_t bytes) {
         return (int)e;
     }
     return 0;
+}
+
+static size_t bcF_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8; }
+
+int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
+    const WGeom& g = a.g;
+    constexpr int kTsz666 = bc::Win<6, 6, 6>::TSZ;
+    MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_fwd (broadcast): compiled for 6^3 windows");
+    const int NHG = heads / 2;
+    a.hsplit = NHG;
+    const size_t lds = bcF_lds();
+    const int grid = bc_blocks(lds, NHG, 4);
+    int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_fwd_bc_kernel<6, 6, 6>), lds);
+    if (rc) return rc;
+    wattn_fwd_bc_kernel<6, 6, 6><<<grid, bc::kThreads, lds, s>>>(a);
+    return launch_status("wattn_fwd_bc");
 }
 
 int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipStream_t s) {

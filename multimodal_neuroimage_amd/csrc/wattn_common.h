@@ -109,6 +109,7 @@ int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, 
 bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind);
 size_t wattn_bc_workspace_bytes(const WGeom& g, int heads);
 int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipStream_t s);
+int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s);   // same geometries; vmax as the packed kernels
 
 // The bias-table gradient is a scatter-add of N*N*heads values per window into a
 // (2w-1)^k x heads table.  LDS float atomics (ds_add_f32) run ~5x slower than the rest of the
