@@ -325,23 +325,55 @@ def mha_core(q, k, v, heads, causal_diag=0, scale=None, dropout=0.0, seed=None):
     return _MHA.apply(q, k, v, heads, causal_diag, scale, float(dropout), int(seed or 0))
 
 
+class _MhaMeanProbs(torch.autograd.Function):
+    """Head-averaged (dropped) probabilities from the kernel's lse.  Forward: the HIP kernel.
+    Backward (rarely needed: no reference caller back-propagates through the weights, but the
+    reference's autograd would): the per-head probabilities are rebuilt on the device in fp32 from
+    q, k and lse, then dS = P (dP - rowsum(dP P)) and dq = scale dS k, dk = scale dS^T q."""
+
+    @staticmethod
+    def forward(ctx, q, k, lse, heads, causal_diag, scale, dropout, seed):
+        Tq, B, E = q.shape
+        Tk = k.shape[0]
+        qc = q if (q.stride(1) == E and q.stride(0) == B * E) else q.contiguous()
+        kc = k if (k.stride(1) == E and k.stride(0) == B * E) else k.contiguous()
+        probs = torch.empty((B, Tq, Tk), device=q.device, dtype=torch.float32)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed, q.dtype)
+        check(_lib.load().mmni_mha_mean_probs(d, ptr(qc), ptr(kc), ptr(lse), ptr(probs), stream_handle(q.device)),
+              "mmni_mha_mean_probs")
+        ctx.save_for_backward(q, k, lse)
+        ctx.cfg = (heads, causal_diag, scale, dropout, seed)
+        return probs
+
+    @staticmethod
+    def backward(ctx, dw):
+        q, k, lse = ctx.saved_tensors
+        heads, diag, scale, dropout, seed = ctx.cfg
+        Tq, B, E = q.shape
+        Tk = k.shape[0]
+        hd = E // heads
+        qh = q.float().reshape(Tq, B, heads, hd).permute(1, 2, 0, 3)     # (B, h, Tq, d)
+        kh = k.float().reshape(Tk, B, heads, hd).permute(1, 2, 0, 3)     # (B, h, Tk, d)
+        s = torch.matmul(qh, kh.transpose(-1, -2)) * scale
+        if diag > 0:
+            s = s + torch.triu(torch.full((Tq, Tk), float("-inf"), device=q.device), diag)
+        p = torch.exp(s - lse.unsqueeze(-1))                              # the forward's softmax
+        dp = (dw.float() / heads).unsqueeze(1).expand(B, heads, Tq, Tk)
+        if dropout > 0:
+            dp = dp * mha_dropout_mask(Tq, Tk, B, heads, dropout, seed, q.device, diag)
+        ds = p * (dp - (dp * p).sum(-1, keepdim=True))
+        dq = (torch.matmul(ds, kh) * scale).permute(2, 0, 1, 3).reshape(Tq, B, E)
+        dk = (torch.matmul(ds.transpose(-1, -2), qh) * scale).permute(2, 0, 1, 3).reshape(Tk, B, E)
+        return dq.to(q.dtype), dk.to(k.dtype), None, None, None, None, None, None
+
+
 def mha_mean_probs(q, k, lse, heads, causal_diag=0, scale=None, dropout=0.0, seed=0):
-    """Head-averaged (dropped) attention weights (B, Tq, Tk) (multihead_attention.py:123,131-133)."""
-    Tq, B, E = q.shape
-    Tk = k.shape[0]
+    """Head-averaged (dropped) attention weights (B, Tq, Tk) (multihead_attention.py:123,131-133),
+    differentiable with respect to q and k."""
+    E = q.shape[-1]
     if scale is None:
         scale = (E // heads) ** -0.5
-    q = q.detach()
-    k = k.detach()
-    if q.stride(1) != E or q.stride(0) != B * E:
-        q = q.contiguous()
-    if k.stride(1) != E or k.stride(0) != B * E:
-        k = k.contiguous()
-    probs = torch.empty((B, Tq, Tk), device=q.device, dtype=torch.float32)
-    d = _mha_desc(Tq, Tk, B, heads, E // heads, causal_diag, scale, E, E, E, E, dropout, seed, q.dtype)
-    check(_lib.load().mmni_mha_mean_probs(d, ptr(q), ptr(k), ptr(lse), ptr(probs), stream_handle(q.device)),
-          "mmni_mha_mean_probs")
-    return probs
+    return _MhaMeanProbs.apply(q, k, lse, heads, causal_diag, scale, float(dropout), int(seed or 0))
 
 
 def mha_dropout_mask(Tq, Tk, B, heads, dropout, seed, device, causal_diag=0):

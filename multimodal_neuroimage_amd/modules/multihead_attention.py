@@ -9,8 +9,9 @@ asked for (need_weights=True, the reference's behaviour); TransformerEncoderLaye
 them, so the encoder never materialises a T x T tensor.  Attention dropout (the reference's
 F.dropout of the probabilities, multihead_attention.py:123; default --attn_dropout 0.1,
 main.py:176) runs inside the kernels from a counter-based mask: one seed per call, drawn from
-torch's default generator, regenerated in the backward.  The weights are not differentiable
-(no caller of the reference back-propagates through them).
+torch's default generator, regenerated in the backward.  The weights are differentiable with
+respect to q and k (their backward rebuilds the per-head probabilities on the device; no caller of
+the reference back-propagates through them, so that path is not optimised).
 """
 import torch
 from torch import nn

@@ -168,6 +168,31 @@ def test_mha_fwd_bwd_vs_oracle(device, Tq, Tk, B, heads, hd, causal):
         assert rel_err(a.grad, b.grad) < TOL
 
 
+@pytest.mark.parametrize("Tq,Tk,causal,p", [(64, 64, True, 0.0), (50, 70, True, 0.0), (64, 64, True, 0.2)])
+def test_mha_mean_weights_gradient_vs_oracle(device, Tq, Tk, causal, p):
+    """The second return value of MultiheadAttention (head-averaged, dropped weights) back-propagates
+    into q and k as the reference's autograd would (multihead_attention.py:123,131-133)."""
+    B, heads, hd = 2, 4, 7
+    E = heads * hd
+    gen = torch.Generator().manual_seed(Tq + Tk)
+    q, k, v = [torch.randn(T, B, E, generator=gen, dtype=torch.float64) for T in (Tq, Tk, Tk)]
+    gw = torch.randn(B, Tq, Tk, generator=gen, dtype=torch.float64)
+    diag = O.causal_diag(Tq, Tk) if causal else 0
+    seed = 1234
+    dm = MF.mha_dropout_mask(Tq, Tk, B, heads, p, seed, device, diag).double().cpu() if p > 0 else None
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    _, ref_w = O.mha_core(*leaves, heads, diag, drop_mask=dm)
+    (ref_w * gw).sum().backward()
+    dev = [t.float().to(device).requires_grad_(True) for t in (q, k, v)]
+    _, lse = MF.mha_core(*dev, heads, diag, dropout=p, seed=seed)
+    w = MF.mha_mean_probs(dev[0], dev[1], lse, heads, diag, dropout=p, seed=seed)
+    (w * gw.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(w, ref_w) < TOL
+    assert rel_err(dev[0].grad, leaves[0].grad) < TOL
+    assert rel_err(dev[1].grad, leaves[1].grad) < TOL
+
+
 MHA_BF16 = [
     # Tq, Tk, B, heads, hd, causal  (C5: bf16 storage, one bf16 product, fp32 accumulation)
     (368, 368, 2, 12, 7, True),
