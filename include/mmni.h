@@ -83,8 +83,12 @@ int mmni_wattn_fwd(const mmni_wattn_desc* d,
  * belongs to exactly one window).  dtable (Tsz, heads) and dtau (heads) are ACCUMULATED
  * (dtable += grad): the caller zeroes them.  dtau may be NULL for kind 0.
  * workspace: >= mmni_wattn_bwd_workspace_bytes(d) bytes, 8-byte aligned, contents ignored
- * (the library zeroes it on the stream); it holds the 64-bit fixed-point table gradient, which
- * makes dtable bitwise deterministic.
+ * (the library initialises what it uses on the stream).  Either path makes dtable bitwise
+ * deterministic:
+ *   - row-broadcast path (kind 0, 6x6x6 windows, C == 2*heads): one fp32 partial table row per
+ *     workgroup (its waves' private LDS copies summed in a fixed order), then a fixed-order
+ *     column sum; vmax is not read;
+ *   - every other shape: a 64-bit fixed-point table gradient with a max|dout|,max|v| bound.
  * vmax (both calls, nullable): one uint32 the caller zeroes before the forward; the forward raises
  * it to the float bits of max|v| over the call (folded into the K/V staging), and the backward
  * then scans only dout for the fixed-point bound instead of dout and v.  ABI v2 added it. */

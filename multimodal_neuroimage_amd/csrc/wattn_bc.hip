@@ -182,14 +182,16 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
 #pragma unroll
             for (int k = 0; k < WW; ++k) {
                 char* pm = trow + (WW - 1 - k) * EB;   // entry E-  (query t, key n + H)
-                f2 nk[2][2], nv[2][2], nm, nz, np;
-                if (k + 1 < WW) fetch(kvr + (k + 1) * 8, trow + (WW - 2 - k) * EB, nk, nv, nm, nz, np);
-                else fetch(kvn, pen, nk, nv, nm, nz, np);
-                // this key's table-gradient entries (after the previous key's stores)
+                // this key's table-gradient entries (after the previous key's stores), read BEFORE
+                // the next key's prefetch: LDS returns in order, so waiting for these then leaves
+                // the prefetch in flight across the step
                 f2* dm = reinterpret_cast<f2*>(pm + DTO);
                 f2* d0 = reinterpret_cast<f2*>(pm + Wn::DC * EB + DTO);
                 f2* dp = reinterpret_cast<f2*>(pm + 2 * Wn::DC * EB + DTO);
                 const f2 om = *dm, o0 = *d0, op = *dp;
+                f2 nk[2][2], nv[2][2], nm, nz, np;
+                if (k + 1 < WW) fetch(kvr + (k + 1) * 8, trow + (WW - 2 - k) * EB, nk, nv, nm, nz, np);
+                else fetch(kvn, pen, nk, nv, nm, nz, np);
                 int rk[2] = {0, 0};
                 if (MASKED) {
                     rk[0] = bc::region_code(reg, i, j, k);
