@@ -121,6 +121,14 @@ __device__ __forceinline__ int region_code(const Regions& r, int i, int j, int k
     return ((i >= r.lz) << 2) | ((j >= r.ly) << 1) | (k >= r.lx);
 }
 
+// The backward may fold p = 2^(s - lse) into 2^s * 2^-lse, with 2^-lse multiplied into dO and
+// -delta once per row, when |lse| (log2 domain) <= kFoldMax for the rows involved: then 2^s <=
+// 2^kFoldMax and 2^-lse >= 2^-kFoldMax, so neither factor over- or underflows where p matters and
+// the per-score subtract disappears.  Rows outside the bound take the subtracting loop.
+constexpr float kFoldMax = 30.0f;
+
+__device__ __forceinline__ bool fold_ok(f2 l) { return fabsf(l.x) <= kFoldMax && fabsf(l.y) <= kFoldMax; }
+
 }  // namespace bc
 
 using bc::f2;
@@ -132,7 +140,7 @@ using bc::Row;
 // LDS tables, TSZ entries of one f2 (the head pair) each: bias * log2 e, then wave 0's and wave
 // 1's table gradients, TSZ * 8 B apart (beyond ds_read2_b64's reach: each access stays one
 // ds_read_b64 / ds_write_b64), all addressed from one lane register plus immediates.
-template <int WD, int WH, int WW, int WAVE, bool MASKED>
+template <int WD, int WH, int WW, int WAVE, bool MASKED, bool FOLD>
 __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2], const f2 (&lse2)[2],
                                           const f2 (&ndl)[2], Row (&dq)[2], int cq, const int (&rq)[2],
                                           const bc::Regions& reg, float* tabdt, const float* kv_s) {
@@ -203,7 +211,7 @@ __device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2],
 #pragma unroll
                     for (int v = 0; v < 2; ++v) {
                         const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
-                        f2 base = t - lse2[u];
+                        f2 base = FOLD ? t : t - lse2[u];   // FOLD: 2^-lse rides in dO and -delta
                         if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
                         f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
                         s = bc::pfma(q[u].x[1], kk[v][1], s);
@@ -286,14 +294,37 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
             }
         }
         __syncthreads();
+        // the lane's rows are its own: the fold is decided per wave (uniform control flow)
+        const bool fold = __all(!lane_ok || (bc::fold_ok(lse2[0]) && bc::fold_ok(lse2[1])));
         if (lane_ok) {
-            if (reg.masked) {
-                if (wave == 0) bwdA_loop<WD, WH, WW, 0, true>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
-                else bwdA_loop<WD, WH, WW, 1, true>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
-            } else {
-                if (wave == 0) bwdA_loop<WD, WH, WW, 0, false>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
-                else bwdA_loop<WD, WH, WW, 1, false>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s);
+            if (fold) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const f2 e = bc::exp2_2(-lse2[u]);
+                    dO[u].x[0] *= e;
+                    dO[u].x[1] *= e;
+                    ndl[u] *= e;
+                }
             }
+#define MMNI_BWDA(W, M, F) bwdA_loop<WD, WH, WW, W, M, F>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s)
+            if (fold) {
+                if (reg.masked) {
+                    if (wave == 0) MMNI_BWDA(0, true, true);
+                    else MMNI_BWDA(1, true, true);
+                } else {
+                    if (wave == 0) MMNI_BWDA(0, false, true);
+                    else MMNI_BWDA(1, false, true);
+                }
+            } else {
+                if (reg.masked) {
+                    if (wave == 0) MMNI_BWDA(0, true, false);
+                    else MMNI_BWDA(1, true, false);
+                } else {
+                    if (wave == 0) MMNI_BWDA(0, false, false);
+                    else MMNI_BWDA(1, false, false);
+                }
+            }
+#undef MMNI_BWDA
 #pragma unroll
             for (int u = 0; u < 2; ++u) bc::store_row_nat(a.dq + row[u] * a.qs + coff, dq[u], a.scale);
         }
@@ -313,7 +344,7 @@ void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
 // ------------------------------------------------------------------------------------
 // pass B: lane = key pair (t, t + H); queries (n, n + H) broadcast; dk, dv
 // ------------------------------------------------------------------------------------
-template <int WD, int WH, int WW, bool MASKED>
+template <int WD, int WH, int WW, bool MASKED, bool FOLD>
 __device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2], Row (&dk)[2], Row (&dv)[2],
                                           int ck, const int (&rk)[2], const bc::Regions& reg, const float* tab_s,
                                           const float* rs_s) {
@@ -342,7 +373,7 @@ __device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2]
                     qq[u][1] = src[1];
                     gg[u][0] = src[2];
                     gg[u][1] = src[3];
-                    ls[u] = src[4];
+                    ls[u] = FOLD ? bc::splat(0.f) : src[4];
                     nd[u] = src[5];
                 }
                 const f2 tbm = *reinterpret_cast<const f2*>(pm);
@@ -358,7 +389,7 @@ __device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2]
 #pragma unroll
                     for (int v = 0; v < 2; ++v) {   // key t + v H
                         const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
-                        f2 base = t - ls[u];
+                        f2 base = FOLD ? t : t - ls[u];
                         if (MASKED) base += bc::splat(rq[u] == rk[v] ? 0.f : kMask2);
                         f2 s = bc::pfma(qq[u][0], kr[v].x[0], base);
                         s = bc::pfma(qq[u][1], kr[v].x[1], s);
@@ -395,40 +426,57 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
     const int coff = it.hp * 4;
     const float qs2 = a.scale * kLog2e;
     for (int w = it.first; w < g.nwin; w += it.stride) {
-        __syncthreads();
         Row kr[2], vr[2], dk[2], dv[2];
         int ck = 0, rk[2] = {0, 0};
         int64_t row[2] = {0, 0};
         const bc::Regions reg = bc::window_regions(g, w);
+        TokenInfo ti[2];
+        f2 l2[2] = {bc::splat(0.f), bc::splat(0.f)};
+        bool bad = false;
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                ti[u] = token_info(g, w, t + u * H);
+                l2[u] = (f2){a.lse[ti[u].row * NHT + 2 * it.hp], a.lse[ti[u].row * NHT + 2 * it.hp + 1]} * kLog2e;
+                bad |= !bc::fold_ok(l2[u]);
+            }
+        }
+        // every wave reads every query record: the fold is decided per window (this barrier also
+        // orders the previous window's record reads before the stores below)
+        const bool fold = !__syncthreads_or(bad);
         if (lane_ok) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int tt = t + u * H;
-                const TokenInfo ti = token_info(g, w, tt);
-                row[u] = ti.row;
+                row[u] = ti[u].row;
                 rk[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
-                if (u == 0) ck = Wn::OFF - ti.code;
-                kr[u] = bc::load_row_pk(a.k + ti.row * a.ks + coff);
-                vr[u] = bc::load_row_pk(a.v + ti.row * a.vs + coff);
+                if (u == 0) ck = Wn::OFF - ti[u].code;
+                kr[u] = bc::load_row_pk(a.k + ti[u].row * a.ks + coff);
+                vr[u] = bc::load_row_pk(a.v + ti[u].row * a.vs + coff);
                 dk[u].x[0] = dk[u].x[1] = dv[u].x[0] = dv[u].x[1] = bc::splat(0.f);
-                const float4 qr = *reinterpret_cast<const float4*>(a.q + ti.row * a.qs + coff);
-                const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti.row * a.os + coff);
-                const float4 orow = *reinterpret_cast<const float4*>(a.o + ti.row * a.os + coff);
-                const float l0 = a.lse[ti.row * NHT + 2 * it.hp], l1 = a.lse[ti.row * NHT + 2 * it.hp + 1];
+                const float4 qr = *reinterpret_cast<const float4*>(a.q + ti[u].row * a.qs + coff);
+                const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti[u].row * a.os + coff);
+                const float4 orow = *reinterpret_cast<const float4*>(a.o + ti[u].row * a.os + coff);
+                const f2 e = fold ? bc::exp2_2(-l2[u]) : bc::splat(1.f);
                 f2* dst = reinterpret_cast<f2*>(rs_s) + t * 12 + u * 6;   // query record t
                 const float d0 = orow.x * gr.x + orow.y * gr.y, d1 = orow.z * gr.z + orow.w * gr.w;
                 dst[0] = (f2){qr.x * qs2, qr.z * qs2};
                 dst[1] = (f2){qr.y * qs2, qr.w * qs2};
-                dst[2] = (f2){gr.x, gr.z};
-                dst[3] = (f2){gr.y, gr.w};
-                dst[4] = (f2){l0 * kLog2e, l1 * kLog2e};
-                dst[5] = (f2){-d0, -d1};
+                dst[2] = (f2){gr.x, gr.z} * e;
+                dst[3] = (f2){gr.y, gr.w} * e;
+                dst[4] = l2[u];
+                dst[5] = (f2){-d0, -d1} * e;
             }
         }
         __syncthreads();
         if (lane_ok) {
-            if (reg.masked) bwdB_loop<WD, WH, WW, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
-            else bwdB_loop<WD, WH, WW, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+            if (fold) {
+                if (reg.masked) bwdB_loop<WD, WH, WW, true, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+                else bwdB_loop<WD, WH, WW, false, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+            } else {
+                if (reg.masked) bwdB_loop<WD, WH, WW, true, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+                else bwdB_loop<WD, WH, WW, false, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 bc::store_row_nat(a.dv + row[u] * a.vs + coff, dv[u], 1.0f);

@@ -134,6 +134,51 @@ def test_window_attention_large_logits_and_masking(device):
     assert rel_err(out, ref) < TOL
 
 
+@pytest.mark.parametrize("cross", [False, True])
+def test_window_attention_backward_large_lse_windows(device, cross):
+    """6^3 kind-0 windows (the row-broadcast kernels) where some rows have |lse| far above the
+    backward's fold bound (kFoldMax = 30 in log2 units) and others below it: both the folded and
+    the subtracting loops run in one call, per wave (pass A) and per window (pass B)."""
+    B, spatial, window, shift, C, heads = 1, (12, 12, 12), (6, 6, 6), (3, 3, 3), 12, 6
+    geom = MF.WindowGeometry(B, spatial, window, shift)
+    gen = torch.Generator().manual_seed(11)
+    rows = geom.tokens
+    q = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    k = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    v = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    q[: rows // 3] *= 40.0          # scores up to ~100 (natural log) in the first third of the volume
+    table = torch.randn(geom.table_rows, heads, generator=gen, dtype=torch.float64) * 0.5
+    table[:, 0] -= 60.0             # head 0: every score shifted down, lse ~ -60
+    gout = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    scale = (C // heads) ** -0.5
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v, table)]
+    ref = O.window_attention(*leaves, B, spatial, window, shift, heads, 0, scale=scale)
+    (ref * gout).sum().backward()
+    f = lambda t: t.float().to(device).requires_grad_(True)  # noqa: E731
+    tab_d = f(table)
+    if cross:
+        qd, kvd = f(q), f(torch.cat([k, v], dim=1))
+        out = MF.window_attention_cross(qd, kvd, tab_d, geom, heads, kind=0, scale=scale)
+    else:
+        qkvd = f(torch.cat([q, k, v], dim=1))
+        out = MF.window_attention_self(qkvd, tab_d, geom, heads, kind=0, scale=scale)
+    (out * gout.float().to(device)).sum().backward()
+    torch.cuda.synchronize()
+    if cross:
+        dq, dk, dv = qd.grad, kvd.grad[:, :C], kvd.grad[:, C:]
+    else:
+        dq, dk, dv = qkvd.grad[:, :C], qkvd.grad[:, C:2 * C], qkvd.grad[:, 2 * C:]
+    assert rel_err(out, ref) < TOL
+    # per head: the scaled third dominates the global maximum, so compare each head's columns
+    # and the unscaled rows on their own scale as well
+    for h in range(heads):
+        cols = slice(2 * h, 2 * h + 2)
+        for got, want in ((dq, leaves[0].grad), (dk, leaves[1].grad), (dv, leaves[2].grad)):
+            assert rel_err(got[:, cols], want[:, cols]) < TOL
+            assert rel_err(got[rows // 3:, cols], want[rows // 3:, cols]) < TOL
+        assert rel_err(tab_d.grad[:, h], leaves[3].grad[:, h]) < TOL
+
+
 MHA = [
     # Tq, Tk, B, heads, hd, causal
     (16, 16, 2, 12, 7, True),
