@@ -22,7 +22,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}",
 
 # Per-file extras.  mlp.hip: keep MFMA accumulators in arch VGPRs (the GELU epilogue reads every
 # accumulator; AGPR accumulators cost a v_accvgpr_read per element — 323 -> 206 VALU per tile).
-EXTRA = {"mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "blockops.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# mha.hip: the softmax reads every score accumulator (196 v_accvgpr moves in the bf16 backward).
+EXTRA = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("mlp.hip", "blockops.hip", "mha.hip")}
 
 
 def sources():

@@ -482,7 +482,13 @@ __device__ __forceinline__ void tile_loop(int tb, int te, Load&& load, Store&& s
 // ------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------
-template <int HDP, bool DROP, typename T>
+// Online softmax with a lazy reference (as the window-attention forward): tile 0 sets each row's
+// reference m to its exact maximum; later tiles start the score accumulator at -m, so p = 2^acc
+// needs no subtract, and m moves (with the rescale of o and l) only when some score of the wave
+// exceeds it by more than kMhaLazy.  So p <= 2^kMhaLazy: no overflow in l, o or the bf16 P.
+constexpr float kMhaLazy = 8.0f;
+
+template <int HDP, bool DROP, typename T, bool ONES>
 __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     constexpr int TERMS = kTerms<T>;
     using G = Geo<HDP, TERMS>;
@@ -503,7 +509,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
         for (int d = 0; d < HDP; ++d) qv[d] = load_pad<T>(a.q, rq, d, a.hd, qok) * a.scale2;
         build_y<HDP, TERMS>(qv, lg, qy);
     }
-    const bool ones = !DROP && a.hd < HDP;   // the denominator as V's padding row of ones (host sets it)
+    // ONES: the denominator rides as V's padding row of ones (the host sets it when !DROP && hd < HDP)
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vzg = a.vz + (int64_t)bh * a.nkt * G::ZT;
@@ -528,10 +534,12 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
             if (k0 >= kend_w) return;   // wave-uniform: every key of the tile is masked for this wave
             const uint16_t* kx = lds + buf * STAGE;
             const uint16_t* vz = kx + SK;
+            // tile 0 is every live wave's first tile (key 0 is visible to every row)
+            const float init = t == 0 ? 0.f : -m;
             mf4 s[4];
 #pragma unroll
-            for (int st = 0; st < 4; ++st) s[st] = sprod<HDP, TERMS>(kx, st, qy, (mf4){0.f, 0.f, 0.f, 0.f}, ln, lg);
-            // lane: s[st][i] = S^T[key k0 + 16 st + 4 lg + i][query qi] (log2 domain)
+            for (int st = 0; st < 4; ++st) s[st] = sprod<HDP, TERMS>(kx, st, qy, (mf4){init, init, init, init}, ln, lg);
+            // lane: s[st][i] = S^T[key k0 + 16 st + 4 lg + i][query qi] - m (log2 domain)
             const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
             if (edge) mask_keys(s, k0, qi, lg, a);
             float mx = -INFINITY;
@@ -539,21 +547,31 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
             for (int st = 0; st < 4; ++st)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[st][i]);
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float mn = fmaxf(m, mx);
-            const float ms = mn == -INFINITY ? 0.f : mn;   // no visible key yet: every p below is 0
-            const float alpha = fast_exp2(m - ms);
-            m = mn;
-            o *= alpha;
-            if (!ones) lsum *= alpha;
+            if (t == 0 || __any(mx > kMhaLazy)) {   // wave-uniform: set or raise the reference
+                mx = fmaxf(mx, __shfl_xor(mx, 16));
+                mx = fmaxf(mx, __shfl_xor(mx, 32));
+                // first tile: the row maximum (0 if no key is visible); later: raise by mx if positive
+                const float d = t == 0 ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
+                if (t == 0) {
+                    m = d;
+                } else {
+                    m += d;
+                    const float alpha = fast_exp2(-d);
+                    o *= alpha;
+                    if (!ONES) lsum *= alpha;
+                }
+#pragma unroll
+                for (int st = 0; st < 4; ++st)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) s[st][i] -= d;
+            }
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float p = fast_exp2(s[st][i] - ms);
+                    const float p = fast_exp2(s[st][i]);
                     float pv = p;
-                    if (!ones) lsum += p;
+                    if (!ONES) lsum += p;
                     if (DROP) pv = drop_keep(rowh, k0 + 16 * st + 4 * lg + i, a.thresh) ? p * a.inv_keep : 0.f;
                     s[st][i] = pv;
                 }
@@ -561,7 +579,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
             o = zprod<HDP, TERMS>(vz, s, o, ln, lg);
         });
     o = zfinish<HDP, TERMS>(o);
-    if (ones) {
+    if (ONES) {
         const int hd = a.hd, src = ((hd >> 2) << 4) + ln, i = hd & 3;
         const float t = i == 0 ? o[0] : (i == 1 ? o[1] : (i == 2 ? o[2] : o[3]));
         lsum = __shfl(t, src);
@@ -953,7 +971,8 @@ static int mha_fwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     a.kx = kx;
     a.vz = vz;
     dim3 grid(a.nqt, a.B * a.H);
-    mha_fwd_mfma_kernel<HDP, DROP, T><<<grid, 256, 0, s>>>(a);
+    if (!DROP && a.hd < HDP) mha_fwd_mfma_kernel<HDP, DROP, T, true><<<grid, 256, 0, s>>>(a);
+    else mha_fwd_mfma_kernel<HDP, DROP, T, false><<<grid, 256, 0, s>>>(a);
     return launch_status("mha_fwd");
 }
 
