@@ -496,8 +496,13 @@ void wattn_bwdB_bc_kernel(WAArgs a) {
 // per CU), and the other waves hide the broadcast reads.
 // ------------------------------------------------------------------------------------
 constexpr float kLazy = 8.0f;
+// Bounded rows skip the reference altogether: when |s| <= |q| max|k| + max|bias| <= kFwdBound for
+// every key of a row (Cauchy-Schwarz on the log2-scaled scores), p = 2^s lies in
+// [2^-kFwdBound, 2^kFwdBound] (masked keys: ~2^-144, i.e. 0) and l, o stay far inside fp32, so the
+// common step is the bare score, one exp, l += p and o += p v.
+constexpr float kFwdBound = 30.0f;
 
-template <int WD, int WH, int WW, bool MASKED>
+template <int WD, int WH, int WW, bool MASKED, bool BOUNDED>
 __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[2], Row (&o)[2], int cq,
                                          const int (&rq)[2], const bc::Regions& reg, const float* tab,
                                          const float* kv_s) {
@@ -520,7 +525,9 @@ __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[
         p_ = *reinterpret_cast<const f2*>(pe + 2 * Wn::DC * EB);
     };
     fetch(kv2, tb + lane_base, kk, vv, tbm, tb0, tbp);
-    {   // the reference: each row's exact maximum over the first key's two rows
+    if (BOUNDED) {
+        m[0] = m[1] = bc::splat(0.f);
+    } else {   // the reference: each row's exact maximum over the first key's two rows
         int rk[2] = {0, 0};
         if (MASKED) {
             rk[0] = bc::region_code(reg, 0, 0, 0);
@@ -559,15 +566,15 @@ __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[
 #pragma unroll
                     for (int v = 0; v < 2; ++v) {
                         const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
-                        f2 base = t - m[u];
+                        f2 base = BOUNDED ? t : t - m[u];
                         if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
                         f2 sv = bc::pfma(q[u].x[0], kk[v][0], base);
                         sv = bc::pfma(q[u].x[1], kk[v][1], sv);
                         s[u][v] = sv;
-                        smax = fmaxf(smax, fmaxf(sv.x, sv.y));
+                        if (!BOUNDED) smax = fmaxf(smax, fmaxf(sv.x, sv.y));
                     }
                 }
-                if (__any(smax > kLazy)) {   // rare: raise the reference of the rows that need it
+                if (!BOUNDED && __any(smax > kLazy)) {   // rare: raise the reference of the rows that need it
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const f2 up = (f2){fmaxf(fmaxf(s[u][0].x, s[u][1].x), 0.f),
@@ -591,6 +598,9 @@ __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[
                         o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
                     }
                 }
+                // the bounded step has no branch: keep the compiler from hoisting the whole row's
+                // broadcast reads (they spill at the 4-wave register budget)
+                if (BOUNDED) __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
@@ -606,11 +616,21 @@ void wattn_fwd_bc_kernel(WAArgs a) {
     const int NHG = a.hsplit, NHT = 2 * NHG;
     float* tab_s = smem;                 // [TSZ] f2: bias * log2e of the head pair
     float* kv_s = tab_s + TSZ * 2;       // [H][8] f2: key records as in pass A
+    float* red = kv_s + H * 16;          // [2 waves][2 heads] max |bias|, then [2][2] max |k|^2
     const bc::Items it = bc::items(NHG);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6;
     const bool lane_ok = tid < H;
     const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab_s[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
+    float tabs = 0.f;   // this thread's entries all belong to head tid & 1 (the stride is even)
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
+        const float x = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
+        tab_s[e] = x;
+        tabs = fmaxf(tabs, fabsf(x));
+    }
+    for (int off = 2; off < 64; off <<= 1) tabs = fmaxf(tabs, __shfl_xor(tabs, off));
+    if ((tid & 63) < 2) red[wave * 2 + (tid & 1)] = tabs;
+    __syncthreads();
+    const f2 tmax = (f2){fmaxf(red[0], red[2]), fmaxf(red[1], red[3])};
     const int coff = it.hp * 4;
     const f2 qscale = bc::splat(a.scale * kLog2e);
     float vabs = 0.f;
@@ -621,6 +641,7 @@ void wattn_fwd_bc_kernel(WAArgs a) {
         int cq = 0, rq[2] = {0, 0};
         int64_t row[2] = {0, 0};
         const bc::Regions reg = bc::window_regions(g, w);
+        f2 kn = bc::splat(0.f);   // max |k|^2 per head over this lane's two keys
         if (lane_ok) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -634,6 +655,7 @@ void wattn_fwd_bc_kernel(WAArgs a) {
                 q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
                 q[u].x[0] *= qscale;
                 q[u].x[1] *= qscale;
+                kn = (f2){fmaxf(kn.x, kr.x * kr.x + kr.y * kr.y), fmaxf(kn.y, kr.z * kr.z + kr.w * kr.w)};
                 vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
                 f2* kv2 = reinterpret_cast<f2*>(kv_s) + t * 8 + u * 4;   // key record t
                 kv2[0] = (f2){kr.x, kr.z};
@@ -644,10 +666,35 @@ void wattn_fwd_bc_kernel(WAArgs a) {
                 o[u].x[0] = o[u].x[1] = bc::splat(0.f);
             }
         }
+        for (int off = 1; off < 64; off <<= 1)
+            kn = (f2){fmaxf(kn.x, __shfl_xor(kn.x, off)), fmaxf(kn.y, __shfl_xor(kn.y, off))};
+        if ((tid & 63) == 0) {
+            red[4 + wave * 2] = kn.x;
+            red[5 + wave * 2] = kn.y;
+        }
         __syncthreads();
+        // per wave: every row within the bound (the previous window's reads of red[4..7] finished
+        // before this window's first barrier)
+        const f2 kmax2 = (f2){fmaxf(red[4], red[6]), fmaxf(red[5], red[7])};
+        bool rows_ok = true;
         if (lane_ok) {
-            if (reg.masked) fwd_loop<WD, WH, WW, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
-            else fwd_loop<WD, WH, WW, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const f2 qn = bc::pfma(q[u].x[0], q[u].x[0], q[u].x[1] * q[u].x[1]);
+                const f2 qk = qn * kmax2;
+                rows_ok = rows_ok && __builtin_sqrtf(qk.x) + tmax.x <= kFwdBound &&
+                          __builtin_sqrtf(qk.y) + tmax.y <= kFwdBound;
+            }
+        }
+        const bool bounded = __all(rows_ok);
+        if (lane_ok) {
+            if (bounded) {
+                if (reg.masked) fwd_loop<WD, WH, WW, true, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+                else fwd_loop<WD, WH, WW, false, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+            } else {
+                if (reg.masked) fwd_loop<WD, WH, WW, true, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+                else fwd_loop<WD, WH, WW, false, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
@@ -710,7 +757,7 @@ static int set_lds_limit(const void* fn, size_t bytes) {
     return 0;
 }
 
-static size_t bcF_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8; }
+static size_t bcF_lds() { return (size_t)bc::Win<6, 6, 6>::TSZ * 2 * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8 + 8 * 4; }
 
 int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     const WGeom& g = a.g;
