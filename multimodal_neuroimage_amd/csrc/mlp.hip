@@ -169,10 +169,23 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
     }
 
     const int64_t tiles = (a.rows + 15) / 16;
+    // the next tile's x and residual are loaded while this tile computes (one tile in flight per
+    // wave otherwise leaves the chain load -> LN -> MFMA -> GELU -> MFMA exposed)
+    float xn[CS] = {0.f, 0.f, 0.f};
+    f4 rn = (f4){0.f, 0.f, 0.f, 0.f};
+    auto fetch = [&](int64_t tile) {
+        const int64_t t0 = tile * 16;
+        io.load_fm(a.x, t0, xn);
+        if (a.res != nullptr && io.row_ok(t0)) rn = *reinterpret_cast<const f4*>(a.res + (t0 + li) * C + 4 * lg);
+    };
+    if (wave < tiles) fetch(wave);
     for (int64_t tile = wave; tile < tiles; tile += nwaves) {
         const int64_t t0 = tile * 16;
         float xb[CS];
-        io.load_fm(a.x, t0, xb);
+#pragma unroll
+        for (int s = 0; s < CS; ++s) xb[s] = xn[s];
+        const f4 rv = rn;
+        if (tile + nwaves < tiles) fetch(tile + nwaves);
         if constexpr (LN) {
             float mean, rstd;
             ln_stats(xb, a.eps, mean, rstd);
@@ -182,7 +195,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
         const bool ok = io.row_ok(t0);
         const int64_t roff = (t0 + li) * C + 4 * lg;
         f4 acc = b2c;
-        if (a.res != nullptr && ok) acc += *reinterpret_cast<const f4*>(a.res + roff);
+        if (a.res != nullptr && ok) acc += rv;
         // three independent accumulator chains (one per hidden tile), summed at the end
         f4 out[HT];
 #pragma unroll

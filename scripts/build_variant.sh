@@ -9,7 +9,7 @@ mkdir -p "$(dirname "$out")" /tmp/mmni_var
 objs=()
 for f in "$R"/multimodal_neuroimage_amd/csrc/*.hip; do
   o=/tmp/mmni_var/$(basename "$f").$$.o
-  extra=""; case "$(basename "$f")" in mlp.hip|blockops.hip) extra="-mllvm -amdgpu-mfma-vgpr-form";; esac
+  extra=""; case "$(basename "$f")" in mlp.hip|blockops.hip|mha.hip) extra="-mllvm -amdgpu-mfma-vgpr-form";; esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -w $extra "$@" -c "$f" -o "$o" &
   objs+=("$o")
 done
