@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t rows, const 
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, float* __restrict__ dx,
                                                             float* __restrict__ part) {
-    __shared__ float red[256];
+    __shared__ float red[4 * 2 * C];   // [wave][2C]
     float gm[C], dg[C], db[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) { gm[c] = gamma[c]; dg[c] = 0.f; db[c] = 0.f; }
@@ -104,17 +104,20 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t rows, const 
         for (int c = 0; c < C; ++c) g[c] = rs * (g[c] * gm[c] - s1 - xv[c] * s2);
         strow<C>(dx + r * C, g);
     }
-    // workgroup partial sums of dgamma / dbeta -> part[blockIdx][2C]  (fixed-order tree)
+    // workgroup partial sums of dgamma / dbeta -> part[blockIdx][2C]: a butterfly over the wave's
+    // lanes (every lane ends with the same, fixed-order sum), then the 4 wave sums in wave order.
+    // (A 256-wide LDS tree per channel cost 2C x 9 barriers: ~110 us for a 108-row C = 48 call.)
+    const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+#pragma unroll
     for (int c = 0; c < 2 * C; ++c) {
-        red[threadIdx.x] = c < C ? dg[c] : db[c - C];
-        __syncthreads();
-        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 2 * C + c] = red[0];
-        __syncthreads();
+        float v = c < C ? dg[c] : db[c - C];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wib * 2 * C + c] = v;
     }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x)
+        part[(int64_t)blockIdx.x * 2 * C + c] = ((red[c] + red[2 * C + c]) + red[4 * C + c]) + red[6 * C + c];
 }
 
 // out[j] = sum_b part[b][j] in a fixed order (columns j >= split go to out2[j - split]);
@@ -356,6 +359,15 @@ extern "C" int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const fl
 
 static int dw_waves() { return 4096; }
 
+// waves of one linear_dw call: at least 16 four-row steps per wave, so short calls (a few hundred
+// rows at the deep Swin-V2 stages) do not reduce 1024 mostly-empty partial rows
+static int dw_waves_for(int64_t rows) {
+    const int64_t steps = (rows + 3) / 4;
+    int64_t w = (steps + 15) / 16;
+    w = (w + 3) / 4 * 4;
+    return (int)(w < 4 ? 4 : (w > dw_waves() ? dw_waves() : w));
+}
+
 extern "C" size_t mmni_linear_dw_workspace_bytes(int N, int K) {
     return (size_t)(dw_waves() / 4) * (N * K + N) * sizeof(float);   // per-block partials
 }
@@ -366,7 +378,7 @@ extern "C" int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_
     MMNI_ARG_CHECK(ldx >= K && lddy >= N, "linear_dw: leading dimensions too small");
     const int NT = (N + 15) / 16, KT = (K + 15) / 16;
     float* part = reinterpret_cast<float*>(workspace);
-    const int waves = dw_waves();
+    const int waves = dw_waves_for(rows);
     const int grid = waves * 64 / 256;
     const int wb = db != nullptr;
     const size_t lds = (size_t)(N * K + N) * sizeof(float);

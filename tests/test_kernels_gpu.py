@@ -334,7 +334,7 @@ def test_conv3d_weight_grad_is_deterministic(device, Cin, Cout, sp, k, pad):
         assert torch.equal(gw, grads[0][0]) and torch.equal(gb, grads[0][1])
 
 
-LN = [(1000, 12), (70001, 12), (513, 24), (4099, 48), (300, 96)]
+LN = [(1000, 12), (70001, 12), (513, 24), (4099, 48), (300, 96), (108, 48), (7, 24)]
 
 
 @pytest.mark.parametrize("rows,C", LN)
@@ -361,7 +361,8 @@ def test_layernorm_fwd_bwd_vs_torch_fp64(device, rows, C):
     assert rel_err(ln.bias.grad, leaves[2].grad) < TOL
 
 
-LIN = [(5000, 12, 36), (4097, 12, 12), (3001, 12, 48), (3001, 48, 12), (2000, 48, 144), (1000, 24, 72), (777, 96, 48)]
+LIN = [(5000, 12, 36), (4097, 12, 12), (3001, 12, 48), (3001, 48, 12), (2000, 48, 144), (1000, 24, 72), (777, 96, 48),
+       (108, 48, 192), (13, 12, 12), (65, 24, 96)]
 
 
 @pytest.mark.parametrize("rows,K,N", LIN)
