@@ -722,6 +722,618 @@ void wattn_fwd_bc_kernel(WAArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// "quad" layout of 6^3 windows: a lane owns the row quad {b, b + 18, b + 108, b + 126} (its
+// (y + 3, z + 3) partners), b = (z', y', x) with z', y' < 3: 54 lanes = one wave per (window, head
+// pair).  The wave walks the 54 key quads in lock step, so each broadcast record (4 keys x k, v)
+// feeds 16 (query, key) pairs instead of 4, and the 16 pairs of a step touch only 9 table entries
+// (relative offsets a * 3 TW + b * 3 TH, a, b in {-1, 0, 1}).  The bases' codes hit each of the 32
+// 8-byte bank pairs once in lanes 0-31 and at most once in lanes 32-53 (kPermQ), so every
+// per-lane table access is conflict-free.  The 9 x 54 entries of one step are pairwise distinct
+// (codes of bases differ by less than 3 in every digit), so the private table read-modify-write
+// of a step never aliases across lanes.
+// ------------------------------------------------------------------------------------
+#ifndef MMNI_Q4_DSADD
+#define MMNI_Q4_DSADD 0   // table gradient by LDS float adds (ds_add_f32) instead of read-modify-write
+#endif
+namespace q4 {
+constexpr int NB = 54;                              // row quads per window
+constexpr int TW = 121, TH = 11, OFF = 665, TSZ = 1331;
+constexpr int EB = 8;                               // table entry: f2 over the head pair
+constexpr int DMIN = 3 * TW + 3 * TH + 5;           // 401: entry offsets D + DMIN - x are >= 0
+constexpr int REC = 128;                            // key-quad record: 4 keys x (k f4, v f4)
+constexpr int KVB = NB * REC;                       // 6912 B of records per wave
+constexpr int WAVES = 4;                            // waves per workgroup (one head pair per workgroup)
+constexpr int TABB = TSZ * EB;                      // 10648 B per table image
+constexpr int TAB = WAVES * KVB;                    // bias table offset (records first: row bases >= 0)
+constexpr int DT = (TAB + TABB + 15) & ~15;         // gradient images, one per wave
+constexpr int LDS_A = DT + WAVES * TABB;            // 80896 B: two workgroups per CU
+constexpr int LDS_F = TAB + TABB;                   // forward: records + bias table
+__constant__ unsigned char kPermQ[NB] = {0,  1,  2,  3,  4,  5,  26, 27, 28, 29, 50, 6,  7,  8,  9,  10, 11, 32,
+                                         33, 34, 35, 39, 12, 13, 14, 15, 16, 17, 21, 22, 23, 44, 18, 19, 20, 24,
+                                         25, 30, 31, 36, 37, 38, 40, 41, 42, 43, 45, 46, 47, 48, 49, 51, 52, 53};
+__device__ __forceinline__ int base_token(int b) { return (b / 18) * 36 + ((b / 6) % 3) * 6 + b % 6; }
+__device__ __forceinline__ int base_code(int b) { return (b / 18) * TW + ((b / 6) % 3) * TH + b % 6; }
+// combo (u, v) of query row u and key row v (bit 0: +3 y, bit 1: +3 z) -> table entry slot e and
+// its code offset D
+constexpr int slot(int u, int v) { return ((u >> 1) - (v >> 1) + 1) * 3 + ((u & 1) - (v & 1) + 1); }
+constexpr int dcode(int e) { return (e / 3 - 1) * 3 * TW + (e % 3 - 1) * 3 * TH; }
+
+// work of one wave: windows w = xcd + 8 j of its head pair (the head-pair workgroups of a window
+// share an XCD's L2)
+struct Work {
+    int hp, j0, dj, xcd;
+};
+__device__ __forceinline__ Work work(int NHG, int wave) {
+    Work k;
+    k.xcd = blockIdx.x & 7;
+    const int slot = blockIdx.x >> 3, nslots = gridDim.x >> 3;
+    k.hp = slot % NHG;
+    const int nblk = (nslots - k.hp + NHG - 1) / NHG;
+    k.j0 = (slot / NHG) * WAVES + wave;
+    k.dj = nblk * WAVES;
+    return k;
+}
+}  // namespace q4
+
+template <bool MASKED, bool FOLD>
+__device__ __forceinline__ void q4A_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
+                                         const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
+                                         const bc::Regions& reg, char* sm, int kvw, int dtw) {
+    using namespace q4;
+    const char* kv = sm + kvw;
+    const char* tb = sm + TAB;
+    // entry of combo slot e at key x of key row (zr, yr): row base + (D_e + DMIN - x) * EB,
+    // row base = (lcode + OFF - DMIN - code0) * EB
+    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
+    f2 kk[4][2], vv[4][2], bt[9];
+    auto fetch = [&](const char* rec, const char* te, f2 (&k_)[4][2], f2 (&v_)[4][2], f2 (&b_)[9]) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), k_[v][0], k_[v][1]);
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), v_[v][0], v_[v][1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) b_[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
+    };
+    fetch(kv, tb + lane_e, kk, vv, bt);
+    for (int zr = 0; zr < 3; ++zr) {
+        for (int yr = 0; yr < 3; ++yr) {
+            const uint32_t trow = lane_e - (uint32_t)((zr * TW + yr * TH) * EB);
+            const char* tp = tb + trow;
+            char* dp = sm + dtw + trow;
+            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
+            const int yn = yr + 1 < 3 ? yr + 1 : 0, zn = yr + 1 < 3 ? zr : zr + 1;
+            const bool last = zn == 3;   // the final row's prefetch re-reads itself (unused)
+            const char* kvn = last ? kvr : kv + (zn * 3 + yn) * 6 * REC;
+            const char* tpn = last ? tp : tb + (lane_e - (uint32_t)((zn * TW + yn * TH) * EB));
+#pragma unroll
+            for (int x = 0; x < 6; ++x) {
+                // this key quad's gradient entries, read before the next quad's prefetch (LDS
+                // returns in order: waiting on these leaves the prefetch in flight)
+                f2 od[9];
+#if MMNI_Q4_DSADD
+#pragma unroll
+                for (int e = 0; e < 9; ++e) od[e] = bc::splat(0.f);
+#else
+#pragma unroll
+                for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (dcode(e) + DMIN - x) * EB);
+#endif
+                f2 nk[4][2], nv[4][2], nb[9];
+                if (x + 1 < 6) fetch(kvr + (x + 1) * REC, tp - (x + 1) * EB, nk, nv, nb);
+                else fetch(kvn, tpn, nk, nv, nb);
+                int rk[4] = {0, 0, 0, 0};
+                if (MASKED) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int e = slot(u, v);
+                        f2 base = FOLD ? bt[e] : bt[e] - lse2[u];   // FOLD: 2^-lse rides in dO and -delta
+                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                        f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                        s = bc::pfma(q[u].x[1], kk[v][1], s);
+                        const f2 p = bc::exp2_2(s);
+                        f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
+                        tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
+                        const f2 ds = p * tt;
+                        dq[u].x[0] = bc::pfma(ds, kk[v][0], dq[u].x[0]);
+                        dq[u].x[1] = bc::pfma(ds, kk[v][1], dq[u].x[1]);
+                        od[e] += ds;
+                    }
+                }
+#if MMNI_Q4_DSADD
+#pragma unroll
+                for (int e = 0; e < 9; ++e) {
+                    float* pe = reinterpret_cast<float*>(dp + (dcode(e) + DMIN - x) * EB);
+                    __hip_atomic_fetch_add(pe, od[e].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(pe + 1, od[e].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#else
+#pragma unroll
+                for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (dcode(e) + DMIN - x) * EB) = od[e];
+                asm volatile("" ::: "memory");   // the next quad's entry reads stay behind these stores
+#endif
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) { kk[v][c] = nk[v][c]; vv[v][c] = nv[v][c]; }
+#pragma unroll
+                for (int e = 0; e < 9; ++e) bt[e] = nb[e];
+            }
+        }
+    }
+}
+
+// pass A, quad layout: 4 waves per workgroup, one head pair per workgroup, each wave one window at
+// a time with its own key records and private table-gradient image; no block barrier in the loop
+// (a wave reads only what it wrote; LDS runs a wave's accesses in order)
+__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void wattn_bwdA_q4_kernel(WAArgs a, float* part) {
+    using namespace q4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* sm = reinterpret_cast<char*>(smem);
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const Work wk = work(NHG, wave);
+    float* tab = reinterpret_cast<float*>(sm + TAB);
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
+    float* dtf = reinterpret_cast<float*>(sm + DT);
+    for (int e = tid; e < WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
+    __syncthreads();
+    const bool lane_ok = lane < NB;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
+    const int tb0 = base_token(beta), lcode = base_code(beta);
+    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
+    const int kvw = wave * KVB, dtw = DT + wave * TABB;
+    const int coff = wk.hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    for (int j = wk.j0;; j += wk.dj) {
+        const int w = wk.xcd + 8 * j;
+        if (w >= g.nwin) break;
+        Row q[4], dO[4], dq[4];
+        f2 lse2[4], ndl[4];
+        int rq[4] = {0, 0, 0, 0};
+        int64_t row[4] = {0, 0, 0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
+                row[u] = ti.row;
+                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
+                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
+                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
+                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
+                char* rec = sm + kvw + beta * REC + u * 32;   // key u of quad beta
+                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
+                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
+                dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
+            }
+        }
+        asm volatile("" ::: "memory");   // the records are written before the walk reads them
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ok = ok && bc::fold_ok(lse2[u]);
+        const bool fold = __all(!lane_ok || ok);
+        if (lane_ok) {
+            if (fold) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const f2 e = bc::exp2_2(-lse2[u]);
+                    dO[u].x[0] *= e;
+                    dO[u].x[1] *= e;
+                    ndl[u] *= e;
+                }
+            }
+#define MMNI_Q4A(M, F) q4A_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw)
+            if (fold) {
+                if (reg.masked) MMNI_Q4A(true, true);
+                else MMNI_Q4A(false, true);
+            } else {
+                if (reg.masked) MMNI_Q4A(true, false);
+                else MMNI_Q4A(false, false);
+            }
+#undef MMNI_Q4A
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bc::store_row_nat(a.dq + row[u] * a.qs + coff, dq[u], a.scale);
+        }
+        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
+    }
+    __syncthreads();
+    // this workgroup's partial row: its head pair's columns (waves 0..3 summed in order), zeros elsewhere
+    float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
+    for (int e = tid; e < TSZ * NHT; e += blockDim.x) {
+        const int r = e / NHT, c = e - r * NHT;
+        float v = 0.f;
+        if ((c >> 1) == wk.hp) {
+            const int o = r * 2 + (c & 1);
+            v = ((dtf[o] + dtf[TSZ * 2 + o]) + dtf[TSZ * 4 + o]) + dtf[TSZ * 6 + o];
+        }
+        prow[e] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// pass B, quad layout: lane = key quad (4 keys), the wave walks the 54 query quads; query records
+// (q * scale * log2 e, dO [* 2^-lse], -delta [* 2^-lse], lse) broadcast from LDS; dk, dv in registers
+// ------------------------------------------------------------------------------------
+#ifndef MMNI_Q4B_UNROLL
+#define MMNI_Q4B_UNROLL 6
+#endif
+namespace q4 {
+constexpr int QREC = 192;                           // query-quad record: 4 x (q f4, dO f4, (-delta, lse) f4)
+constexpr int QRB = NB * QREC;                      // 10368 B per wave
+constexpr int TAB_B = WAVES * QRB;                  // bias table after the records (row bases >= 0)
+constexpr int LDS_B = TAB_B + TABB;                 // 52120 B: three workgroups per CU
+}  // namespace q4
+
+template <bool MASKED, bool FOLD>
+__device__ __forceinline__ void q4B_loop(const Row (&kr)[4], const Row (&vr)[4], Row (&dk)[4], Row (&dv)[4],
+                                         int lcode, const int (&rk)[4], const bc::Regions& reg, const char* sm,
+                                         int qrw) {
+    using namespace q4;
+    const char* qr = sm + qrw;
+    // entry of (query quad m, row u; key row v) = code(m) - code(beta) + OFF + D(u, v); per query
+    // row (zr, yr) one base, immediates (D + DMIN + x) * EB per query x
+    const uint32_t lane_e = (uint32_t)((OFF - lcode - DMIN) * EB);
+    for (int zr = 0; zr < 3; ++zr) {
+        for (int yr = 0; yr < 3; ++yr) {
+            const char* tp = sm + TAB_B + (lane_e + (uint32_t)((zr * TW + yr * TH) * EB));
+            const char* qrr = qr + (zr * 3 + yr) * 6 * QREC;
+#if MMNI_Q4B_UNROLL == 1
+#pragma unroll 1
+#elif MMNI_Q4B_UNROLL == 2
+#pragma unroll 2
+#elif MMNI_Q4B_UNROLL == 3
+#pragma unroll 3
+#else
+#pragma unroll
+#endif
+            for (int x = 0; x < 6; ++x) {
+                const char* rec = qrr + x * QREC;
+                f2 bt[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(tp + (dcode(e) + DMIN + x) * EB);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {       // query row u of the quad: record (q, dO, -delta, lse)
+                    f2 qq[2], gg[2], nd, ls;
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48), qq[0], qq[1]);
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48 + 16), gg[0], gg[1]);
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48 + 32), nd, ls);
+                    int rq = 0;
+                    if (MASKED) rq = bc::region_code(reg, zr + 3 * (u >> 1), yr + 3 * (u & 1), x);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {   // the lane's key row v
+                        const int e = slot(u, v);
+                        f2 base = FOLD ? bt[e] : bt[e] - ls;
+                        if (MASKED) base += bc::splat(rq == rk[v] ? 0.f : kMask2);
+                        f2 s = bc::pfma(qq[0], kr[v].x[0], base);
+                        s = bc::pfma(qq[1], kr[v].x[1], s);
+                        const f2 p = bc::exp2_2(s);
+                        f2 tt = bc::pfma(gg[0], vr[v].x[0], nd);
+                        tt = bc::pfma(gg[1], vr[v].x[1], tt);
+                        const f2 dsv = p * tt;
+                        dv[v].x[0] = bc::pfma(p, gg[0], dv[v].x[0]);
+                        dv[v].x[1] = bc::pfma(p, gg[1], dv[v].x[1]);
+                        dk[v].x[0] = bc::pfma(dsv, qq[0], dk[v].x[0]);
+                        dk[v].x[1] = bc::pfma(dsv, qq[1], dk[v].x[1]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+#ifndef MMNI_Q4B_WPE
+#define MMNI_Q4B_WPE 2   // waves per SIMD of the quad pass B (3: 168 VGPRs, spills; measured slower)
+#endif
+__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(MMNI_Q4B_WPE)))
+void wattn_bwdB_q4_kernel(WAArgs a) {
+    using namespace q4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* sm = reinterpret_cast<char*>(smem);
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const Work wk = work(NHG, wave);
+    float* tab = reinterpret_cast<float*>(sm + TAB_B);
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
+    __syncthreads();
+    const bool lane_ok = lane < NB;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
+    const int tb0 = base_token(beta), lcode = base_code(beta);
+    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
+    const int qrw = wave * QRB;
+    const int coff = wk.hp * 4;
+    const float qs2 = a.scale * kLog2e;
+    for (int j = wk.j0;; j += wk.dj) {
+        const int w = wk.xcd + 8 * j;
+        if (w >= g.nwin) break;
+        Row kr[4], vr[4], dk[4], dv[4];
+        int rk[4] = {0, 0, 0, 0};
+        int64_t row[4] = {0, 0, 0, 0};
+        f2 l2[4];
+        const bc::Regions reg = bc::window_regions(g, w);
+        bool ok = true;
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
+                row[u] = ti.row;
+                rk[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
+                l2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
+                ok = ok && bc::fold_ok(l2[u]);
+            }
+        }
+        // the lanes' rows are the whole window: the fold is decided per wave = per window
+        const bool fold = __all(!lane_ok || ok);
+        if (lane_ok) {
+            char* rec = sm + qrw + beta * QREC;   // query quad beta
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                kr[u] = bc::load_row_pk(a.k + row[u] * a.ks + coff);
+                vr[u] = bc::load_row_pk(a.v + row[u] * a.vs + coff);
+                dk[u].x[0] = dk[u].x[1] = dv[u].x[0] = dv[u].x[1] = bc::splat(0.f);
+                const float4 qv = *reinterpret_cast<const float4*>(a.q + row[u] * a.qs + coff);
+                const float4 gv = *reinterpret_cast<const float4*>(a.dout + row[u] * a.os + coff);
+                const float4 ov = *reinterpret_cast<const float4*>(a.o + row[u] * a.os + coff);
+                const f2 e = fold ? bc::exp2_2(-l2[u]) : bc::splat(1.f);
+                const float d0 = ov.x * gv.x + ov.y * gv.y, d1 = ov.z * gv.z + ov.w * gv.w;
+                *reinterpret_cast<bc::f4*>(rec + u * 48) = (bc::f4){qv.x * qs2, qv.z * qs2, qv.y * qs2, qv.w * qs2};
+                *reinterpret_cast<bc::f4*>(rec + u * 48 + 16) =
+                    (bc::f4){gv.x * e.x, gv.z * e.y, gv.y * e.x, gv.w * e.y};
+                *reinterpret_cast<bc::f4*>(rec + u * 48 + 32) = (bc::f4){-d0 * e.x, -d1 * e.y, l2[u].x, l2[u].y};
+            }
+        }
+        asm volatile("" ::: "memory");   // the records are written before the walk reads them
+        if (lane_ok) {
+            if (fold) {
+                if (reg.masked) q4B_loop<true, true>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
+                else q4B_loop<false, true>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
+            } else {
+                if (reg.masked) q4B_loop<true, false>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
+                else q4B_loop<false, false>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                bc::store_row_nat(a.dv + row[u] * a.vs + coff, dv[u], 1.0f);
+                bc::store_row_nat(a.dk + row[u] * a.ks + coff, dk[u], kLn2);   // staged q2 = q * scale * log2e
+            }
+        }
+        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// forward, quad layout: lane = query quad, key-quad records (k, v) broadcast as in pass A; online
+// softmax as wattn_fwd_bc_kernel (bounded waves: no reference; others: lazy reference)
+// ------------------------------------------------------------------------------------
+template <bool MASKED, bool BOUNDED>
+__device__ __forceinline__ void q4F_loop(const Row (&q)[4], f2 (&m)[4], f2 (&l)[4], Row (&o)[4], int lcode,
+                                         const int (&rq)[4], const bc::Regions& reg, const char* sm, int kvw) {
+    using namespace q4;
+    const char* kv = sm + kvw;
+    const char* tb = sm + TAB;
+    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
+    f2 kk[4][2], vv[4][2], bt[9];
+    auto fetch = [&](const char* rec, const char* te) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), kk[v][0], kk[v][1]);
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), vv[v][0], vv[v][1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
+    };
+    if (BOUNDED) {
+        m[0] = m[1] = m[2] = m[3] = bc::splat(0.f);
+    } else {   // the reference: each row's exact maximum over key quad 0
+        fetch(kv, tb + lane_e);
+        int rk[4] = {0, 0, 0, 0};
+        if (MASKED) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, 3 * (v >> 1), 3 * (v & 1), 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f2 mx = bc::splat(-INFINITY);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                f2 base = bt[slot(u, v)];
+                if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                s = bc::pfma(q[u].x[1], kk[v][1], s);
+                mx = (f2){fmaxf(mx.x, s.x), fmaxf(mx.y, s.y)};
+            }
+            m[u] = mx;
+        }
+    }
+    for (int zr = 0; zr < 3; ++zr) {
+        for (int yr = 0; yr < 3; ++yr) {
+            const char* tp = tb + (lane_e - (uint32_t)((zr * TW + yr * TH) * EB));
+            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
+#pragma unroll
+            for (int x = 0; x < 6; ++x) {
+                fetch(kvr + x * REC, tp - x * EB);
+                int rk[4] = {0, 0, 0, 0};
+                if (MASKED) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
+                }
+                if (BOUNDED) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            f2 base = bt[slot(u, v)];
+                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                            f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                            s = bc::pfma(q[u].x[1], kk[v][1], s);
+                            const f2 p = bc::exp2_2(s);
+                            l[u] += p;
+                            o[u].x[0] = bc::pfma(p, vv[v][0], o[u].x[0]);
+                            o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
+                        }
+                    }
+                    // no branch in the step: keep the compiler from hoisting the next reads (spills)
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    f2 s[4][4];
+                    float smax = -INFINITY;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            f2 base = bt[slot(u, v)] - m[u];
+                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                            f2 sv = bc::pfma(q[u].x[0], kk[v][0], base);
+                            s[u][v] = bc::pfma(q[u].x[1], kk[v][1], sv);
+                            smax = fmaxf(smax, fmaxf(s[u][v].x, s[u][v].y));
+                        }
+                    }
+                    if (__any(smax > kLazy)) {   // rare: raise the reference of the rows that need it
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            f2 up = bc::splat(0.f);
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) up = (f2){fmaxf(up.x, s[u][v].x), fmaxf(up.y, s[u][v].y)};
+                            const f2 alpha = bc::exp2_2(-up);
+                            l[u] *= alpha;
+                            o[u].x[0] *= alpha;
+                            o[u].x[1] *= alpha;
+                            m[u] += up;
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) s[u][v] -= up;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const f2 p = bc::exp2_2(s[u][v]);
+                            l[u] += p;
+                            o[u].x[0] = bc::pfma(p, vv[v][0], o[u].x[0]);
+                            o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
+void wattn_fwd_q4_kernel(WAArgs a) {
+    using namespace q4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* sm = reinterpret_cast<char*>(smem);
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const Work wk = work(NHG, wave);
+    float* tab = reinterpret_cast<float*>(sm + TAB);
+    float tabs = 0.f;   // this thread's entries all belong to head tid & 1 (the stride is even)
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
+        const float x = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
+        tab[e] = x;
+        tabs = fmaxf(tabs, fabsf(x));
+    }
+    for (int off = 2; off < 64; off <<= 1) tabs = fmaxf(tabs, __shfl_xor(tabs, off));
+    float* red = reinterpret_cast<float*>(sm + LDS_F);   // [WAVES][2] max |bias| per head
+    if (lane < 2) red[wave * 2 + lane] = tabs;
+    __syncthreads();
+    f2 tmax = bc::splat(0.f);
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) tmax = (f2){fmaxf(tmax.x, red[2 * i]), fmaxf(tmax.y, red[2 * i + 1])};
+    const bool lane_ok = lane < NB;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
+    const int tb0 = base_token(beta), lcode = base_code(beta);
+    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
+    const int kvw = wave * KVB;
+    const int coff = wk.hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    float vabs = 0.f;
+    for (int j = wk.j0;; j += wk.dj) {
+        const int w = wk.xcd + 8 * j;
+        if (w >= g.nwin) break;
+        Row q[4], o[4];
+        f2 m[4], l[4];
+        int rq[4] = {0, 0, 0, 0};
+        int64_t row[4] = {0, 0, 0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+        f2 kn = bc::splat(0.f);   // max |k|^2 per head over the lane's keys
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
+                row[u] = ti.row;
+                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
+                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                kn = (f2){fmaxf(kn.x, kr.x * kr.x + kr.y * kr.y), fmaxf(kn.y, kr.z * kr.z + kr.w * kr.w)};
+                vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
+                char* rec = sm + kvw + beta * REC + u * 32;
+                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
+                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
+                l[u] = bc::splat(0.f);
+                o[u].x[0] = o[u].x[1] = bc::splat(0.f);
+            }
+        }
+        asm volatile("" ::: "memory");   // the records are written before the walk reads them
+        for (int off = 1; off < 64; off <<= 1)
+            kn = (f2){fmaxf(kn.x, __shfl_xor(kn.x, off)), fmaxf(kn.y, __shfl_xor(kn.y, off))};
+        bool rows_ok = true;
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const f2 qn = bc::pfma(q[u].x[0], q[u].x[0], q[u].x[1] * q[u].x[1]);
+                const f2 qk = qn * kn;
+                rows_ok = rows_ok && __builtin_sqrtf(qk.x) + tmax.x <= kFwdBound &&
+                          __builtin_sqrtf(qk.y) + tmax.y <= kFwdBound;
+            }
+        }
+        const bool bounded = __all(rows_ok);
+        if (lane_ok) {
+            if (bounded) {
+                if (reg.masked) q4F_loop<true, true>(q, m, l, o, lcode, rq, reg, sm, kvw);
+                else q4F_loop<false, true>(q, m, l, o, lcode, rq, reg, sm, kvw);
+            } else {
+                if (reg.masked) q4F_loop<true, false>(q, m, l, o, lcode, rq, reg, sm, kvw);
+                else q4F_loop<false, false>(q, m, l, o, lcode, rq, reg, sm, kvw);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
+                Row r;
+                r.x[0] = o[u].x[0] * inv;
+                r.x[1] = o[u].x[1] * inv;
+                bc::store_row_nat(a.out + row[u] * a.os + coff, r, 1.0f);
+                a.lse[row[u] * NHT + 2 * wk.hp] = (m[u].x + fast_log2(l[u].x)) * kLn2;
+                a.lse[row[u] * NHT + 2 * wk.hp + 1] = (m[u].y + fast_log2(l[u].y)) * kLn2;
+            }
+        }
+        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
+    }
+    if (a.vmax != nullptr) {
+        for (int off = 32; off > 0; off >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, off));
+        if (lane == 0) atomicMax(a.vmax, __float_as_uint(vabs));
+    }
+}
+
 __global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < n) dtable[e] += src[e];
@@ -751,8 +1363,29 @@ static int bc_blocks(size_t lds, int NHG, int waves_per_eu) {
     return grid < 8 * NHG ? 8 * NHG : grid;
 }
 
+#ifndef MMNI_BWDA_Q4
+#define MMNI_BWDA_Q4 1   // pass A in the quad layout (0: the row-pair kernel)
+#endif
+
+#ifndef MMNI_BWDB_Q4
+#define MMNI_BWDB_Q4 1   // pass B in the quad layout
+#endif
+#ifndef MMNI_FWD_Q4
+#define MMNI_FWD_Q4 0    // forward in the quad layout (measured 5% slower than the row-pair kernel)
+#endif
+
+// quad kernels: per_cu resident 4-wave workgroups per CU (pass A: 2 by LDS; pass B and the
+// forward: 3 by registers), a multiple of 8 with every head pair served
+static int q4_blocks(int per_cu, int NHG) {
+    int grid = per_cu * kNumCU;
+    grid -= grid % 8;
+    return grid < 8 * NHG ? 8 * NHG : grid;
+}
+
+static int bwdA_grid(int NHG) { return MMNI_BWDA_Q4 ? q4_blocks(2, NHG) : bc_blocks(bcA_lds(), NHG, 2); }
+
 size_t wattn_bc_workspace_bytes(const WGeom& g, int heads) {
-    const int gridA = bc_blocks(bcA_lds(), heads / 2, 2);
+    const int gridA = bwdA_grid(heads / 2);
     return ((size_t)gridA + 1) * g.Tsz * heads * sizeof(float);
 }
 
@@ -774,6 +1407,12 @@ int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_fwd (broadcast): compiled for 6^3 windows");
     const int NHG = heads / 2;
     a.hsplit = NHG;
+    if (MMNI_FWD_Q4) {
+        const size_t lds = (size_t)q4::LDS_F + 8 * sizeof(float);
+        const int grid = q4_blocks(3, NHG);
+        wattn_fwd_q4_kernel<<<grid, q4::WAVES * 64, lds, s>>>(a);
+        return launch_status("wattn_fwd_q4");
+    }
     const size_t lds = bcF_lds();
     const int grid = bc_blocks(lds, NHG, 4);
     int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_fwd_bc_kernel<6, 6, 6>), lds);
@@ -789,20 +1428,23 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     const int NHG = heads / 2;
     a.hsplit = NHG;
     const size_t ldsA = bcA_lds(), ldsB = bcB_lds();
-    const int gridA = bc_blocks(ldsA, NHG, 2), gridB = bc_blocks(ldsB, NHG, 3);
-    const void* kA = reinterpret_cast<const void*>(&wattn_bwdA_bc_kernel<6, 6, 6>);
+    const int gridA = bwdA_grid(NHG), gridB = MMNI_BWDB_Q4 ? q4_blocks(MMNI_Q4B_WPE, NHG) : bc_blocks(ldsB, NHG, 3);
+    const void* kA = MMNI_BWDA_Q4 ? reinterpret_cast<const void*>(&wattn_bwdA_q4_kernel)
+                                  : reinterpret_cast<const void*>(&wattn_bwdA_bc_kernel<6, 6, 6>);
     const void* kB = reinterpret_cast<const void*>(&wattn_bwdB_bc_kernel<6, 6, 6>);
-    int rc = set_lds_limit(kA, ldsA);
+    int rc = set_lds_limit(kA, MMNI_BWDA_Q4 ? (size_t)q4::LDS_A : ldsA);
     if (rc) return rc;
-    rc = set_lds_limit(kB, ldsB);
+    rc = MMNI_BWDB_Q4 ? 0 : set_lds_limit(kB, ldsB);
     if (rc) return rc;
     const int ncol = g.Tsz * heads;
     float* part = static_cast<float*>(workspace);          // [gridA][Tsz * heads]
     float* sum = part + (size_t)gridA * ncol;              // [Tsz * heads]
-    wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
+    if (MMNI_BWDA_Q4) wattn_bwdA_q4_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
+    else wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
     rc = launch_status("wattn_bwdA_bc");
     if (rc) return rc;
-    wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
+    if (MMNI_BWDB_Q4) wattn_bwdB_q4_kernel<<<gridB, q4::WAVES * 64, q4::LDS_B, s>>>(a);
+    else wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
     rc = launch_status("wattn_bwdB_bc");
     if (rc) return rc;
     column_sum(part, gridA, ncol, sum, ncol, nullptr, s);
