@@ -965,6 +965,288 @@ void wattn_bwdA_q4_kernel(WAArgs a, float* part) {
 }
 
 // ------------------------------------------------------------------------------------
+// merged backward, quad layout: pass A's walk (lane = query quad, key quads broadcast) also forms
+// the key side.  Per step a lane holds, for the 4 keys of the quad, its partial dk and dv over its
+// 4 query rows: 32 floats = 16 f2 over the head pair, value i = kind * 16 + v * 4 + c * 2 + h
+// (kind 0 dk, 1 dv; key v, dim c, head h).  A fixed butterfly over the 64 lanes (v_permlane32_swap,
+// v_permlane16_swap, then DPP row_ror:8 / row_half_mirror / quad xor 2 / xor 1) leaves lane l with
+// the full sum of value l >> 1, which lane l (even) stores.  Every key quad is visited once per
+// window, so those sums are final: no dk/dv accumulation, and p, ds are formed once per (query,
+// key) instead of once in each pass.  Deterministic (fixed lane tree, fixed row order).
+// ------------------------------------------------------------------------------------
+#ifndef MMNI_Q4M_UNROLL
+#define MMNI_Q4M_UNROLL 1   // unroll the merged walk's key loop
+#endif
+#ifndef MMNI_Q4M_PIPE
+#define MMNI_Q4M_PIPE 0     // issue the next key quad's records during the lane reduction
+#endif
+namespace q4 {
+// The spare lanes (54..63) of the merged walk run every step with zero dO, delta and q (so their
+// ds and partials are exactly 0) and read-modify-write table entries at this code: 6 is no
+// c_r + a * 3 TW + b * 3 TH (|a|, |b| <= 2) for any row-quad code c_r, so within one step their
+// entries never meet a real lane's, and they write back the values they read.  No branch.
+constexpr int kSpareCode = 6;
+__constant__ unsigned char kInvPermQ[NB] = {0, 1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 22, 23, 24, 25, 26, 27, 32, 33, 34, 28, 29, 30, 35, 36, 6, 7, 8, 9, 37, 38, 17, 18, 19, 20, 39, 40, 41, 21, 42, 43, 44, 45, 31, 46, 47, 48, 49, 50, 10, 51, 52, 53};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+
+// 16 f2 partials per lane -> lane l returns the 64-lane sum of value l >> 1
+__device__ __forceinline__ float reduce32(f2 (&P)[16], int lane) {
+    f2 R[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // lanes 0-31 keep f2 k (dk), lanes 32-63 f2 k + 8 (dv)
+        float a0 = P[k].x, b0 = P[k + 8].x, a1 = P[k].y, b1 = P[k + 8].y;
+        swap32(a0, b0);
+        swap32(a1, b1);
+        R[k] = (f2){a0, a1} + (f2){b0, b1};
+    }
+    f2 S[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // rows 0, 2 keep k (keys 0, 1), rows 1, 3 keep k + 4 (keys 2, 3)
+        float a0 = R[k].x, b0 = R[k + 4].x, a1 = R[k].y, b1 = R[k + 4].y;
+        swap16(a0, b0);
+        swap16(a1, b1);
+        S[k] = (f2){a0, a1} + (f2){b0, b1};
+    }
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+    f2 T[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // lane bit 3: key 0 or 1 of the pair (row_ror:8 partner = lane ^ 8)
+        const f2 keep = b3 ? S[k + 2] : S[k], send = b3 ? S[k] : S[k + 2];
+        T[k] = keep + (f2){dpp<0x128>(send.x), dpp<0x128>(send.y)};
+    }
+    // lane bit 2: dim c (row_half_mirror partner = lane ^ 7 within 8)
+    const f2 keep = b2 ? T[1] : T[0], send = b2 ? T[0] : T[1];
+    const f2 U = keep + (f2){dpp<0x141>(send.x), dpp<0x141>(send.y)};
+    // lane bit 1: head h (quad partner lane ^ 2), then lane ^ 1
+    const float kv = b1 ? U.y : U.x, sv = b1 ? U.x : U.y;
+    const float V = kv + dpp<0x4E>(sv);
+    return V + dpp<0xB1>(V);
+}
+}  // namespace q4
+
+template <bool MASKED, bool FOLD>
+__device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
+                                         const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
+                                         const bc::Regions& reg, char* sm, int kvw, int dtw, bool lane_ok,
+                                         const int (&rowk)[4], float* kout, int64_t kstride, float kscale) {
+    using namespace q4;
+    const int lane = threadIdx.x & 63;
+    const char* kv = sm + kvw;
+    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
+    const int vsel = (lane >> 3) & 3;   // the key whose sum this lane ends with (l >> 1 = kind, v, c, h)
+    // MMNI_Q4M_PIPE: after a step's table stores, the next step's records and bias entries are
+    // issued and the step's lane reduction (pure VALU) runs while they are in flight.  The table
+    // base goes through an empty asm after the stores, so the compiler treats the next step's table
+    // reads as possibly aliasing them (other lanes' entries) and keeps them behind the stores; LDS
+    // executes a wave's accesses in order, so no wait is needed.
+    f2 kk[4][2], vv[4][2], bt[9], od[9];
+    auto load = [&](const char* rec, const char* te) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), kk[v][0], kk[v][1]);
+            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), vv[v][0], vv[v][1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
+    };
+    int dto = dtw;   // this wave's table-gradient image (an LDS offset: the accesses stay ds_*)
+    if (MMNI_Q4M_PIPE) load(kv, sm + TAB + lane_e);
+    for (int zr = 0; zr < 3; ++zr) {
+        for (int yr = 0; yr < 3; ++yr) {
+            const uint32_t trow = lane_e - (uint32_t)((zr * TW + yr * TH) * EB);
+            const int yn = yr + 1 < 3 ? yr + 1 : 0, zn = yr + 1 < 3 ? zr : zr + 1;
+            const bool last = zn == 3;   // the final row's prefetch re-reads itself (unused)
+            const uint32_t trown = last ? trow : lane_e - (uint32_t)((zn * TW + yn * TH) * EB);
+            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
+            const char* kvn = last ? kvr : kv + (zn * 3 + yn) * 6 * REC;
+#pragma unroll
+            for (int x = 0; x < 6; ++x) {
+                // spare lanes skip the step (a divergent branch here measured spill-free; without it
+                // the compiler spilled ~800 VGPRs) and contribute zero partials
+                f2 P[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) P[i] = bc::splat(0.f);
+                if (lane_ok) {
+                    char* dp = sm + dto + trow;
+                    // this step's table-gradient entries (after the previous step's stores: see dto)
+#pragma unroll
+                    for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (dcode(e) + DMIN - x) * EB);
+                    if (!MMNI_Q4M_PIPE) load(kvr + x * REC, sm + TAB + trow - x * EB);
+                    int rk[4] = {0, 0, 0, 0};
+                    if (MASKED) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const int e = slot(u, v);
+                            f2 base = FOLD ? bt[e] : bt[e] - lse2[u];
+                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                            f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
+                            s = bc::pfma(q[u].x[1], kk[v][1], s);
+                            const f2 p = bc::exp2_2(s);
+                            f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
+                            tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
+                            const f2 ds = p * tt;
+                            dq[u].x[0] = bc::pfma(ds, kk[v][0], dq[u].x[0]);
+                            dq[u].x[1] = bc::pfma(ds, kk[v][1], dq[u].x[1]);
+                            od[e] += ds;
+                            if (u == 0) {   // first row: plain products (P is zero)
+                                P[v * 2] = ds * q[0].x[0];              // dk, dim 0
+                                P[v * 2 + 1] = ds * q[0].x[1];          // dk, dim 1
+                                P[8 + v * 2] = p * dO[0].x[0];          // dv, dim 0
+                                P[8 + v * 2 + 1] = p * dO[0].x[1];      // dv, dim 1
+                            } else {
+                                P[v * 2] = bc::pfma(ds, q[u].x[0], P[v * 2]);
+                                P[v * 2 + 1] = bc::pfma(ds, q[u].x[1], P[v * 2 + 1]);
+                                P[8 + v * 2] = bc::pfma(p, dO[u].x[0], P[8 + v * 2]);
+                                P[8 + v * 2 + 1] = bc::pfma(p, dO[u].x[1], P[8 + v * 2 + 1]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (dcode(e) + DMIN - x) * EB) = od[e];
+                }
+                asm volatile("" : "+v"(dto));   // next reads: behind the stores above (see the top)
+                __builtin_amdgcn_sched_barrier(0);   // keep later steps' loads from being hoisted (registers)
+                if (MMNI_Q4M_PIPE) {
+                    if (x + 1 < 6) load(kvr + (x + 1) * REC, sm + TAB + trow - (x + 1) * EB);
+                    else load(kvn, sm + TAB + trown);
+                }
+                // all 64 lanes take part in the reduction (spare lanes contribute zeros)
+                const float sum = reduce32(P, lane);
+                // rows of key quad n = (zr, yr, x): held by the lane that owns query quad n
+                const int owner = kInvPermQ[(zr * 3 + yr) * 6 + x];
+                const int r0 = __builtin_amdgcn_readlane(rowk[0], owner), r1 = __builtin_amdgcn_readlane(rowk[1], owner);
+                const int r2 = __builtin_amdgcn_readlane(rowk[2], owner), r3 = __builtin_amdgcn_readlane(rowk[3], owner);
+                const int r = vsel == 0 ? r0 : (vsel == 1 ? r1 : (vsel == 2 ? r2 : r3));
+                if ((lane & 1) == 0) kout[(int64_t)r * kstride] = sum * kscale;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+}
+
+// merged backward: dq, dk, dv and the table gradient in one walk (4 waves per workgroup as pass A)
+__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
+    using namespace q4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* sm = reinterpret_cast<char*>(smem);
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const Work wk = work(NHG, wave);
+    float* tab = reinterpret_cast<float*>(sm + TAB);
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
+    float* dtf = reinterpret_cast<float*>(sm + DT);
+    for (int e = tid; e < WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
+    __syncthreads();
+    const bool lane_ok = lane < NB;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;   // spare lanes run the walk on zero rows
+    const int tb0 = base_token(beta), lcode = lane_ok ? base_code(beta) : kSpareCode;
+    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
+    const int kvw = wave * KVB, dtw = DT + wave * TABB;
+    const int coff = wk.hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    // this lane's output slot of the key-side sums: value l >> 1 = (kind, key, dim c, head h)
+    const bool is_dv = lane & 32;
+    const int comp = ((lane >> 1) & 1) * 2 + ((lane >> 2) & 1);   // global row order (h0c0, h0c1, h1c0, h1c1)
+    float* kout = (is_dv ? a.dv : a.dk) + coff + comp;
+    const int64_t kstride = is_dv ? a.vs : a.ks;
+    const float kscale = is_dv ? 1.0f : kLn2;   // dk: the staged q carries scale * log2 e
+    for (int j = wk.j0;; j += wk.dj) {
+        const int w = wk.xcd + 8 * j;
+        if (w >= g.nwin) break;
+        Row q[4], dO[4], dq[4];
+        f2 lse2[4], ndl[4];
+        int rq[4] = {0, 0, 0, 0}, rowk[4] = {0, 0, 0, 0};
+        const bc::Regions reg = bc::window_regions(g, w);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            q[u].x[0] = q[u].x[1] = dO[u].x[0] = dO[u].x[1] = dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
+            lse2[u] = ndl[u] = bc::splat(0.f);
+        }
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
+                rowk[u] = (int)ti.row;
+                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
+                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
+                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
+                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
+                char* rec = sm + kvw + beta * REC + u * 32;   // key u of quad beta
+                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
+                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
+            }
+        }
+        asm volatile("" ::: "memory");   // the records are written before the walk reads them
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ok = ok && bc::fold_ok(lse2[u]);
+        const bool fold = __all(ok);
+        if (fold) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const f2 e = bc::exp2_2(-lse2[u]);
+                dO[u].x[0] *= e;
+                dO[u].x[1] *= e;
+                ndl[u] *= e;
+            }
+        }
+#define MMNI_Q4M(M, F) \
+    q4M_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw, lane_ok, rowk, kout, kstride, kscale)
+        if (fold) {
+            if (reg.masked) MMNI_Q4M(true, true);
+            else MMNI_Q4M(false, true);
+        } else {
+            if (reg.masked) MMNI_Q4M(true, false);
+            else MMNI_Q4M(false, false);
+        }
+#undef MMNI_Q4M
+        if (lane_ok) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bc::store_row_nat(a.dq + (int64_t)rowk[u] * a.qs + coff, dq[u], a.scale);
+        }
+        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
+    }
+    __syncthreads();
+    float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
+    for (int e = tid; e < TSZ * NHT; e += blockDim.x) {
+        const int r = e / NHT, c = e - r * NHT;
+        float v = 0.f;
+        if ((c >> 1) == wk.hp) {
+            const int o = r * 2 + (c & 1);
+            v = ((dtf[o] + dtf[TSZ * 2 + o]) + dtf[TSZ * 4 + o]) + dtf[TSZ * 6 + o];
+        }
+        prow[e] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // pass B, quad layout: lane = key quad (4 keys), the wave walks the 54 query quads; query records
 // (q * scale * log2 e, dO [* 2^-lse], -delta [* 2^-lse], lse) broadcast from LDS; dk, dv in registers
 // ------------------------------------------------------------------------------------
@@ -1382,7 +1664,13 @@ static int q4_blocks(int per_cu, int NHG) {
     return grid < 8 * NHG ? 8 * NHG : grid;
 }
 
-static int bwdA_grid(int NHG) { return MMNI_BWDA_Q4 ? q4_blocks(2, NHG) : bc_blocks(bcA_lds(), NHG, 2); }
+#ifndef MMNI_BWD_MERGED
+#define MMNI_BWD_MERGED 1   // one merged quad kernel (dq, dk, dv, table) instead of passes A and B
+#endif
+
+static int bwdA_grid(int NHG) {
+    return (MMNI_BWDA_Q4 || MMNI_BWD_MERGED) ? q4_blocks(2, NHG) : bc_blocks(bcA_lds(), NHG, 2);
+}
 
 size_t wattn_bc_workspace_bytes(const WGeom& g, int heads) {
     const int gridA = bwdA_grid(heads / 2);
@@ -1439,14 +1727,22 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     const int ncol = g.Tsz * heads;
     float* part = static_cast<float*>(workspace);          // [gridA][Tsz * heads]
     float* sum = part + (size_t)gridA * ncol;              // [Tsz * heads]
-    if (MMNI_BWDA_Q4) wattn_bwdA_q4_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
-    else wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
-    rc = launch_status("wattn_bwdA_bc");
-    if (rc) return rc;
-    if (MMNI_BWDB_Q4) wattn_bwdB_q4_kernel<<<gridB, q4::WAVES * 64, q4::LDS_B, s>>>(a);
-    else wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
-    rc = launch_status("wattn_bwdB_bc");
-    if (rc) return rc;
+    if (MMNI_BWD_MERGED) {
+        rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_bwd_q4m_kernel), q4::LDS_A);
+        if (rc) return rc;
+        wattn_bwd_q4m_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
+        rc = launch_status("wattn_bwd_q4m");
+        if (rc) return rc;
+    } else {
+        if (MMNI_BWDA_Q4) wattn_bwdA_q4_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
+        else wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
+        rc = launch_status("wattn_bwdA_bc");
+        if (rc) return rc;
+        if (MMNI_BWDB_Q4) wattn_bwdB_q4_kernel<<<gridB, q4::WAVES * 64, q4::LDS_B, s>>>(a);
+        else wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
+        rc = launch_status("wattn_bwdB_bc");
+        if (rc) return rc;
+    }
     column_sum(part, gridA, ncol, sum, ncol, nullptr, s);
     rc = launch_status("wattn_bwd_dtable_sum");
     if (rc) return rc;
