@@ -1,31 +1,29 @@
-// Window-attention backward for head_dim 2, "row-broadcast" formulation (SURVEY §8 rows a1, a3;
-// reference: WindowAttention_fusion.forward swinfusion_module.py:114-145 and
-// Cross_WindowAttention.forward :213-246, whose autograd backward this replaces).
+// Window attention for head_dim 2 on 6^3 windows, kind 0 (reference:
+// WindowAttention_fusion.forward swinfusion_module.py:114-145 and Cross_WindowAttention.forward
+// :213-246, and the autograd backward of both).  Head pairs are packed into f2 lanes of
+// v_pk_fma_f32 (head 0, head 1), so a wave works on one head pair of one window at a time.
 //
-// Two kernels per call, one workgroup = one (window, head pair) at a time, persistent:
-//   pass A  (wattn_bwdA_bc_kernel)  lane = query pair (t, t + N/2)  ->  dq and the bias-table gradient
-//   pass B  (wattn_bwdB_bc_kernel)  lane = key pair   (t, t + N/2)  ->  dk and dv
-// Every lane of a wave walks the SAME other-side row pair at each step (keys in pass A, queries in
-// pass B): those rows are LDS broadcast reads, and the per-lane work per (query, key, head pair)
-// is the bare recompute + gradient on packed fp32: no online reductions, no cross-lane traffic.
+//   forward   wattn_fwd_bc_kernel   lane = query pair (t, t + N/2); the wave walks the keys in
+//                                   lock step, each key record an LDS broadcast read; online softmax
+//   backward  wattn_bwd_q4m_kernel  lane = query quad (y + 3, z + 3 partners); the wave walks the
+//                                   54 key quads; per step p and ds of 16 (query, key) pairs give
+//                                   dq (registers), the bias-table gradient (private LDS image) and
+//                                   dk / dv partials that a 64-lane butterfly reduces to the final
+//                                   sums of the step's 4 keys -- one pass, no recomputation
 //
-// LDS facts that shape it (measured here, gfx950): a same-address ds_read_b128 does NOT broadcast
-// (it ran ~16x slower than 8-byte broadcasts), so broadcast rows are stored as 8-byte component
-// arrays ([component][row] f2) read by ds_read_b64 / ds_read2_b64.  The window is a compile-time shape (6^3 at the C3 geometry), so
-// the key/query coordinates and codes are scalar loop counters, and every table access of a step
-// is one address register plus immediate offsets.
+// LDS facts that shape them (measured here, gfx950): a broadcast record is read 16 bytes at a time
+// from a 16-byte-aligned address (ds_read_b128: 4 LDS cycles; the compiler's ds_read2_b64 pairs take
+// 8; a misaligned b128 ran ~16x slower).  The window is a compile-time shape, so the key/query
+// coordinates and codes are scalar loop counters, and every table access of a step is one address
+// register plus immediate offsets.
 //
 // Bias-table gradient without atomics.  At one step the wave's lanes hold distinct queries against
-// the same key pair, so the relative-position entries they update, code(q) - code(k) + off, are
-// pairwise distinct (with the paired rows: entries E0, E0 - d, E0 + d, d = code(N/2), and no two
-// lanes' sets intersect because no two of their queries are N/2 apart).  Each wave therefore
-// read-modify-writes its OWN fp32 copy of the table in LDS with plain loads and stores: no atomics,
-// no fixed-point scale, no max|dO| pre-pass.  A workgroup always serves the same head pair; its
-// waves' copies are summed in a fixed order at the end into one partial row per workgroup, and a
-// fixed-order column sum (tokenops.hip) adds the rows: bitwise deterministic.
-//
-// Kind 0 only (scaled dot + table bias), one head pair (4 channels) per workgroup, windows with an
-// even first extent (N/2 = whole planes).
+// the same keys, so the relative-position entries they update, code(q) - code(k) + off, are
+// pairwise distinct.  Each wave therefore read-modify-writes its OWN fp32 copy of the table in LDS
+// with plain loads and stores: no atomics, no fixed-point scale, no max|dO| pre-pass (LDS float
+// atomics measured ~8x slower).  A workgroup always serves the same head pair; its waves' copies
+// are summed in a fixed order into one partial row per workgroup, and a fixed-order column sum
+// (tokenops.hip) adds the rows: bitwise deterministic.
 #include "wattn_common.h"
 
 namespace mmni {
@@ -145,357 +143,6 @@ __device__ __forceinline__ bool fold_ok(f2 l) { return fabsf(l.x) <= kFoldMax &&
 
 using bc::f2;
 using bc::Row;
-
-// ------------------------------------------------------------------------------------
-// pass A: lane = query pair (t, t + H); keys (n, n + H) broadcast; dq + private table gradient
-// ------------------------------------------------------------------------------------
-// LDS tables, TSZ entries of one f2 (the head pair) each: bias * log2 e, then wave 0's and wave
-// 1's table gradients, TSZ * 8 B apart (beyond ds_read2_b64's reach: each access stays one
-// ds_read_b64 / ds_write_b64), all addressed from one lane register plus immediates.
-template <int WD, int WH, int WW, int WAVE, bool MASKED, bool FOLD>
-__device__ __forceinline__ void bwdA_loop(const Row (&q)[2], const Row (&dO)[2], const f2 (&lse2)[2],
-                                          const f2 (&ndl)[2], Row (&dq)[2], int cq, const int (&rq)[2],
-                                          const bc::Regions& reg, float* tabdt, const float* kv_s) {
-    using Wn = bc::Win<WD, WH, WW>;
-    constexpr int EB = 8;                           // entry bytes
-    constexpr int DTO = (1 + WAVE) * Wn::TSZ * EB;  // this wave's table gradient
-    char* tb = reinterpret_cast<char*>(tabdt);
-    // lane address of entry (cq - code(n) - DC) = E- for code(n) = 0; E0 / E+ at +DC / +2 DC entries
-    const uint32_t lane_base = (uint32_t)((cq - Wn::DC) * EB);
-    const f2* kv2 = reinterpret_cast<const f2*>(kv_s);
-    // Software pipeline: the broadcast K/V rows and the (read-only) bias entries of key n + 1 are
-    // loaded during key n.  The private-table read-modify-write is the one ordered access: lanes
-    // share entries across consecutive keys (lane t at key n + 1 reads what lane t - 1 wrote at
-    // key n), a cross-lane order the compiler cannot see, so a compiler barrier after each key's
-    // table stores keeps every later table read behind them (LDS executes a wave's accesses in
-    // order; no wait is needed).
-    // Keys are walked row by row (a row = WW consecutive keys, fixed (i, j)).  Per row one uniform
-    // base addresses the broadcast K/V records and one lane base the table entries, so every
-    // per-key access below is a base register plus an immediate offset (no per-key address math):
-    // record of key n at kv2[8 n] (k c0, k c1, v c0, v c1 of key n, then of key n + H); entries of
-    // key k of the row at trow + (WW - 1 - k) EB, trow = lane_base - (code0 + WW - 1) EB.
-    f2 kk[2][2], vv[2][2], tbm, tb0, tbp;
-    auto fetch = [&](const f2* kvk, const char* pe, f2 (&k_)[2][2], f2 (&v_)[2][2], f2& m_, f2& z_, f2& p_) {
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            bc::ld_pair(kvk + v * 4, k_[v][0], k_[v][1]);
-            bc::ld_pair(kvk + v * 4 + 2, v_[v][0], v_[v][1]);
-        }
-        m_ = *reinterpret_cast<const f2*>(pe);
-        z_ = *reinterpret_cast<const f2*>(pe + Wn::DC * EB);
-        p_ = *reinterpret_cast<const f2*>(pe + 2 * Wn::DC * EB);
-    };
-    fetch(kv2, tb + lane_base, kk, vv, tbm, tb0, tbp);
-    for (int i = 0; i < WD / 2; ++i) {
-        for (int j = 0; j < WH; ++j) {
-            const int code0 = i * Wn::TW + j * Wn::TH;
-            const f2* kvr = kv2 + (i * WH + j) * WW * 8;
-            char* trow = tb + (lane_base - (uint32_t)((code0 + WW - 1) * EB));
-            // the next row's bases, for the prefetch at the row's last key (the final row re-reads
-            // itself: valid, unused data)
-            const int jn = j + 1 < WH ? j + 1 : 0, in = j + 1 < WH ? i : i + 1;
-            const bool last = in == WD / 2;
-            const f2* kvn = last ? kvr : kv2 + (in * WH + jn) * WW * 8;
-            const char* pen = last ? trow : tb + (lane_base - (uint32_t)((in * Wn::TW + jn * Wn::TH) * EB));
-#pragma unroll
-            for (int k = 0; k < WW; ++k) {
-                char* pm = trow + (WW - 1 - k) * EB;   // entry E-  (query t, key n + H)
-                // this key's table-gradient entries (after the previous key's stores), read BEFORE
-                // the next key's prefetch: LDS returns in order, so waiting for these then leaves
-                // the prefetch in flight across the step
-                f2* dm = reinterpret_cast<f2*>(pm + DTO);
-                f2* d0 = reinterpret_cast<f2*>(pm + Wn::DC * EB + DTO);
-                f2* dp = reinterpret_cast<f2*>(pm + 2 * Wn::DC * EB + DTO);
-                const f2 om = *dm, o0 = *d0, op = *dp;
-                f2 nk[2][2], nv[2][2], nm, nz, np;
-                if (k + 1 < WW) fetch(kvr + (k + 1) * 8, trow + (WW - 2 - k) * EB, nk, nv, nm, nz, np);
-                else fetch(kvn, pen, nk, nv, nm, nz, np);
-                int rk[2] = {0, 0};
-                if (MASKED) {
-                    rk[0] = bc::region_code(reg, i, j, k);
-                    rk[1] = bc::region_code(reg, i + WD / 2, j, k);
-                }
-                f2 ds[2][2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                    for (int v = 0; v < 2; ++v) {
-                        const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
-                        f2 base = FOLD ? t : t - lse2[u];   // FOLD: 2^-lse rides in dO and -delta
-                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                        f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
-                        s = bc::pfma(q[u].x[1], kk[v][1], s);
-                        const f2 p = bc::exp2_2(s);
-                        f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
-                        tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
-                        ds[u][v] = p * tt;
-                        dq[u].x[0] = bc::pfma(ds[u][v], kk[v][0], dq[u].x[0]);
-                        dq[u].x[1] = bc::pfma(ds[u][v], kk[v][1], dq[u].x[1]);
-                    }
-                }
-                // private table: no two lanes of the wave share an entry at one key
-                *d0 = o0 + (ds[0][0] + ds[1][1]);
-                *dm = om + ds[0][1];
-                *dp = op + ds[1][0];
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int v = 0; v < 2; ++v)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) { kk[v][c] = nk[v][c]; vv[v][c] = nv[v][c]; }
-                tbm = nm;
-                tb0 = nz;
-                tbp = np;
-            }
-        }
-    }
-}
-
-template <int WD, int WH, int WW>
-__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(2)))
-void wattn_bwdA_bc_kernel(WAArgs a, float* part) {
-    using Wn = bc::Win<WD, WH, WW>;
-    constexpr int H = Wn::H, TSZ = Wn::TSZ;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    float* tabdt = smem;                          // [3][TSZ] f2: bias pair, dt wave 0, dt wave 1
-    float* kv_s = tabdt + bc::align4(TSZ * 6);    // [H][8] f2: k c0, k c1, v c0, v c1 of key n, then of n + H
-    const bc::Items it = bc::items(NHG);
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const bool lane_ok = tid < H;
-    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
-        tabdt[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
-        tabdt[TSZ * 2 + e] = 0.f;
-        tabdt[TSZ * 4 + e] = 0.f;
-    }
-    const int coff = it.hp * 4;
-    const f2 qscale = bc::splat(a.scale * kLog2e);
-    for (int w = it.first; w < g.nwin; w += it.stride) {
-        __syncthreads();   // previous window's K/V reads done (and the table staged, first time)
-        Row q[2], dO[2], dq[2];
-        f2 lse2[2], ndl[2];
-        int cq = 0, rq[2] = {0, 0};
-        int64_t row[2] = {0, 0};
-        const bc::Regions reg = bc::window_regions(g, w);
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int tt = t + u * H;
-                const TokenInfo ti = token_info(g, w, tt);
-                row[u] = ti.row;
-                rq[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
-                if (u == 0) cq = ti.code + Wn::OFF;
-                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
-                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
-                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
-                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
-                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
-                q[u].x[0] *= qscale;
-                q[u].x[1] *= qscale;
-                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
-                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * it.hp], a.lse[ti.row * NHT + 2 * it.hp + 1]} * kLog2e;
-                f2* kv2 = reinterpret_cast<f2*>(kv_s) + t * 8 + u * 4;   // key record t
-                kv2[0] = (f2){kr.x, kr.z};
-                kv2[1] = (f2){kr.y, kr.w};
-                kv2[2] = (f2){vr.x, vr.z};
-                kv2[3] = (f2){vr.y, vr.w};
-                dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
-            }
-        }
-        __syncthreads();
-        // the lane's rows are its own: the fold is decided per wave (uniform control flow)
-        const bool fold = __all(!lane_ok || (bc::fold_ok(lse2[0]) && bc::fold_ok(lse2[1])));
-        if (lane_ok) {
-            if (fold) {
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const f2 e = bc::exp2_2(-lse2[u]);
-                    dO[u].x[0] *= e;
-                    dO[u].x[1] *= e;
-                    ndl[u] *= e;
-                }
-            }
-#define MMNI_BWDA(W, M, F) bwdA_loop<WD, WH, WW, W, M, F>(q, dO, lse2, ndl, dq, cq, rq, reg, tabdt, kv_s)
-            if (fold) {
-                if (reg.masked) {
-                    if (wave == 0) MMNI_BWDA(0, true, true);
-                    else MMNI_BWDA(1, true, true);
-                } else {
-                    if (wave == 0) MMNI_BWDA(0, false, true);
-                    else MMNI_BWDA(1, false, true);
-                }
-            } else {
-                if (reg.masked) {
-                    if (wave == 0) MMNI_BWDA(0, true, false);
-                    else MMNI_BWDA(1, true, false);
-                } else {
-                    if (wave == 0) MMNI_BWDA(0, false, false);
-                    else MMNI_BWDA(1, false, false);
-                }
-            }
-#undef MMNI_BWDA
-#pragma unroll
-            for (int u = 0; u < 2; ++u) bc::store_row_nat(a.dq + row[u] * a.qs + coff, dq[u], a.scale);
-        }
-    }
-    __syncthreads();
-    // this workgroup's partial row: its head pair's columns (wave 0 + wave 1, fixed order), zeros in
-    // the other head pairs' columns
-    float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
-    for (int e = tid; e < TSZ * NHT; e += blockDim.x) {
-        const int r = e / NHT, c = e - r * NHT;
-        float v = 0.f;
-        if ((c >> 1) == it.hp) v = tabdt[TSZ * 2 + r * 2 + (c & 1)] + tabdt[TSZ * 4 + r * 2 + (c & 1)];
-        prow[e] = v;
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// pass B: lane = key pair (t, t + H); queries (n, n + H) broadcast; dk, dv
-// ------------------------------------------------------------------------------------
-template <int WD, int WH, int WW, bool MASKED, bool FOLD>
-__device__ __forceinline__ void bwdB_loop(const Row (&kr)[2], const Row (&vr)[2], Row (&dk)[2], Row (&dv)[2],
-                                          int ck, const int (&rk)[2], const bc::Regions& reg, const float* tab_s,
-                                          const float* rs_s) {
-    using Wn = bc::Win<WD, WH, WW>;
-    constexpr int EB = 8;
-    const char* tb = reinterpret_cast<const char*>(tab_s);
-    // entry of (query n, key t) = code(n) + ck, ck = OFF - code(t); (n, t + H) is DC lower,
-    // (n + H, t) DC higher
-    const uint32_t lane_base = (uint32_t)((ck - Wn::DC) * EB);
-    // query records rs2[12 n]: q2 c0, q2 c1, dO c0, dO c1 of query n, the same of n + H, then -delta
-    // of n and n + H, lse2 of n and n + H (16-byte groups);
-    // per row one base each for the records and the table entries, immediates per query
-    const f2* rs2 = reinterpret_cast<const f2*>(rs_s);
-    for (int i = 0; i < WD / 2; ++i) {
-        for (int j = 0; j < WH; ++j) {
-            const int code0 = i * Wn::TW + j * Wn::TH;
-            const f2* rsr = rs2 + (i * WH + j) * WW * 12;
-            const char* trow = tb + (lane_base + (uint32_t)(code0 * EB));
-#pragma unroll 3   // fully unrolled, the hoisted record loads spill at the 3-wave budget
-            for (int k = 0; k < WW; ++k) {
-                const char* pm = trow + k * EB;   // (n, t + H)
-                f2 qq[2][2], gg[2][2], ls[2], nd[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const f2* src = rsr + k * 12 + u * 4;
-                    bc::ld_pair(src, qq[u][0], qq[u][1]);
-                    bc::ld_pair(src + 2, gg[u][0], gg[u][1]);
-                }
-                bc::ld_pair(rsr + k * 12 + 8, nd[0], nd[1]);
-                if (FOLD) ls[0] = ls[1] = bc::splat(0.f);
-                else bc::ld_pair(rsr + k * 12 + 10, ls[0], ls[1]);
-                const f2 tbm = *reinterpret_cast<const f2*>(pm);
-                const f2 tb0 = *reinterpret_cast<const f2*>(pm + Wn::DC * EB);
-                const f2 tbp = *reinterpret_cast<const f2*>(pm + 2 * Wn::DC * EB);
-                int rq[2] = {0, 0};
-                if (MASKED) {
-                    rq[0] = bc::region_code(reg, i, j, k);
-                    rq[1] = bc::region_code(reg, i + WD / 2, j, k);
-                }
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {       // query n + u H
-#pragma unroll
-                    for (int v = 0; v < 2; ++v) {   // key t + v H
-                        const f2 t = (u == v) ? tb0 : (u == 0 ? tbm : tbp);
-                        f2 base = FOLD ? t : t - ls[u];
-                        if (MASKED) base += bc::splat(rq[u] == rk[v] ? 0.f : kMask2);
-                        f2 s = bc::pfma(qq[u][0], kr[v].x[0], base);
-                        s = bc::pfma(qq[u][1], kr[v].x[1], s);
-                        const f2 p = bc::exp2_2(s);
-                        f2 tt = bc::pfma(gg[u][0], vr[v].x[0], nd[u]);
-                        tt = bc::pfma(gg[u][1], vr[v].x[1], tt);
-                        const f2 dsv = p * tt;
-                        dv[v].x[0] = bc::pfma(p, gg[u][0], dv[v].x[0]);
-                        dv[v].x[1] = bc::pfma(p, gg[u][1], dv[v].x[1]);
-                        dk[v].x[0] = bc::pfma(dsv, qq[u][0], dk[v].x[0]);
-                        dk[v].x[1] = bc::pfma(dsv, qq[u][1], dk[v].x[1]);
-                    }
-                }
-            }
-        }
-    }
-}
-
-template <int WD, int WH, int WW>
-__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(3)))
-void wattn_bwdB_bc_kernel(WAArgs a) {
-    using Wn = bc::Win<WD, WH, WW>;
-    constexpr int H = Wn::H, TSZ = Wn::TSZ;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    float* tab_s = smem;                            // [TSZ][2] bias * log2e of the head pair
-    float* rs_s = tab_s + bc::align4(TSZ * 2);      // [H][12] f2: (q2 c0, q2 c1, dO c0, dO c1) x 2, -delta x 2, lse2 x 2
-    const bc::Items it = bc::items(NHG);
-    const int tid = threadIdx.x;
-    const bool lane_ok = tid < H;
-    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab_s[e] = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
-    const int coff = it.hp * 4;
-    const float qs2 = a.scale * kLog2e;
-    for (int w = it.first; w < g.nwin; w += it.stride) {
-        Row kr[2], vr[2], dk[2], dv[2];
-        int ck = 0, rk[2] = {0, 0};
-        int64_t row[2] = {0, 0};
-        const bc::Regions reg = bc::window_regions(g, w);
-        TokenInfo ti[2];
-        f2 l2[2] = {bc::splat(0.f), bc::splat(0.f)};
-        bool bad = false;
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                ti[u] = token_info(g, w, t + u * H);
-                l2[u] = (f2){a.lse[ti[u].row * NHT + 2 * it.hp], a.lse[ti[u].row * NHT + 2 * it.hp + 1]} * kLog2e;
-                bad |= !bc::fold_ok(l2[u]);
-            }
-        }
-        // every wave reads every query record: the fold is decided per window (this barrier also
-        // orders the previous window's record reads before the stores below)
-        const bool fold = !__syncthreads_or(bad);
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int tt = t + u * H;
-                row[u] = ti[u].row;
-                rk[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
-                if (u == 0) ck = Wn::OFF - ti[u].code;
-                kr[u] = bc::load_row_pk(a.k + ti[u].row * a.ks + coff);
-                vr[u] = bc::load_row_pk(a.v + ti[u].row * a.vs + coff);
-                dk[u].x[0] = dk[u].x[1] = dv[u].x[0] = dv[u].x[1] = bc::splat(0.f);
-                const float4 qr = *reinterpret_cast<const float4*>(a.q + ti[u].row * a.qs + coff);
-                const float4 gr = *reinterpret_cast<const float4*>(a.dout + ti[u].row * a.os + coff);
-                const float4 orow = *reinterpret_cast<const float4*>(a.o + ti[u].row * a.os + coff);
-                const f2 e = fold ? bc::exp2_2(-l2[u]) : bc::splat(1.f);
-                f2* rec = reinterpret_cast<f2*>(rs_s) + t * 12;   // query record t
-                f2* dst = rec + u * 4;
-                const float d0 = orow.x * gr.x + orow.y * gr.y, d1 = orow.z * gr.z + orow.w * gr.w;
-                dst[0] = (f2){qr.x * qs2, qr.z * qs2};
-                dst[1] = (f2){qr.y * qs2, qr.w * qs2};
-                dst[2] = (f2){gr.x, gr.z} * e;
-                dst[3] = (f2){gr.y, gr.w} * e;
-                rec[8 + u] = (f2){-d0, -d1} * e;
-                rec[10 + u] = l2[u];
-            }
-        }
-        __syncthreads();
-        if (lane_ok) {
-            if (fold) {
-                if (reg.masked) bwdB_loop<WD, WH, WW, true, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
-                else bwdB_loop<WD, WH, WW, false, true>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
-            } else {
-                if (reg.masked) bwdB_loop<WD, WH, WW, true, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
-                else bwdB_loop<WD, WH, WW, false, false>(kr, vr, dk, dv, ck, rk, reg, tab_s, rs_s);
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                bc::store_row_nat(a.dv + row[u] * a.vs + coff, dv[u], 1.0f);
-                bc::store_row_nat(a.dk + row[u] * a.ks + coff, dk[u], kLn2);   // staged q2 = q * scale * log2e
-            }
-        }
-    }
-}
 
 // ------------------------------------------------------------------------------------
 // forward: lane = query pair (t, t + H); keys (n, n + H) broadcast from LDS as in pass A.
@@ -733,9 +380,6 @@ void wattn_fwd_bc_kernel(WAArgs a) {
 // (codes of bases differ by less than 3 in every digit), so the private table read-modify-write
 // of a step never aliases across lanes.
 // ------------------------------------------------------------------------------------
-#ifndef MMNI_Q4_DSADD
-#define MMNI_Q4_DSADD 0   // table gradient by LDS float adds (ds_add_f32) instead of read-modify-write
-#endif
 namespace q4 {
 constexpr int NB = 54;                              // row quads per window
 constexpr int TW = 121, TH = 11, OFF = 665, TSZ = 1331;
@@ -748,7 +392,6 @@ constexpr int TABB = TSZ * EB;                      // 10648 B per table image
 constexpr int TAB = WAVES * KVB;                    // bias table offset (records first: row bases >= 0)
 constexpr int DT = (TAB + TABB + 15) & ~15;         // gradient images, one per wave
 constexpr int LDS_A = DT + WAVES * TABB;            // 80896 B: two workgroups per CU
-constexpr int LDS_F = TAB + TABB;                   // forward: records + bias table
 __constant__ unsigned char kPermQ[NB] = {0,  1,  2,  3,  4,  5,  26, 27, 28, 29, 50, 6,  7,  8,  9,  10, 11, 32,
                                          33, 34, 35, 39, 12, 13, 14, 15, 16, 17, 21, 22, 23, 44, 18, 19, 20, 24,
                                          25, 30, 31, 36, 37, 38, 40, 41, 42, 43, 45, 46, 47, 48, 49, 51, 52, 53};
@@ -776,194 +419,6 @@ __device__ __forceinline__ Work work(int NHG, int wave) {
 }
 }  // namespace q4
 
-template <bool MASKED, bool FOLD>
-__device__ __forceinline__ void q4A_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
-                                         const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
-                                         const bc::Regions& reg, char* sm, int kvw, int dtw) {
-    using namespace q4;
-    const char* kv = sm + kvw;
-    const char* tb = sm + TAB;
-    // entry of combo slot e at key x of key row (zr, yr): row base + (D_e + DMIN - x) * EB,
-    // row base = (lcode + OFF - DMIN - code0) * EB
-    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
-    f2 kk[4][2], vv[4][2], bt[9];
-    auto fetch = [&](const char* rec, const char* te, f2 (&k_)[4][2], f2 (&v_)[4][2], f2 (&b_)[9]) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), k_[v][0], k_[v][1]);
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), v_[v][0], v_[v][1]);
-        }
-#pragma unroll
-        for (int e = 0; e < 9; ++e) b_[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
-    };
-    fetch(kv, tb + lane_e, kk, vv, bt);
-    for (int zr = 0; zr < 3; ++zr) {
-        for (int yr = 0; yr < 3; ++yr) {
-            const uint32_t trow = lane_e - (uint32_t)((zr * TW + yr * TH) * EB);
-            const char* tp = tb + trow;
-            char* dp = sm + dtw + trow;
-            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
-            const int yn = yr + 1 < 3 ? yr + 1 : 0, zn = yr + 1 < 3 ? zr : zr + 1;
-            const bool last = zn == 3;   // the final row's prefetch re-reads itself (unused)
-            const char* kvn = last ? kvr : kv + (zn * 3 + yn) * 6 * REC;
-            const char* tpn = last ? tp : tb + (lane_e - (uint32_t)((zn * TW + yn * TH) * EB));
-#pragma unroll
-            for (int x = 0; x < 6; ++x) {
-                // this key quad's gradient entries, read before the next quad's prefetch (LDS
-                // returns in order: waiting on these leaves the prefetch in flight)
-                f2 od[9];
-#if MMNI_Q4_DSADD
-#pragma unroll
-                for (int e = 0; e < 9; ++e) od[e] = bc::splat(0.f);
-#else
-#pragma unroll
-                for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (dcode(e) + DMIN - x) * EB);
-#endif
-                f2 nk[4][2], nv[4][2], nb[9];
-                if (x + 1 < 6) fetch(kvr + (x + 1) * REC, tp - (x + 1) * EB, nk, nv, nb);
-                else fetch(kvn, tpn, nk, nv, nb);
-                int rk[4] = {0, 0, 0, 0};
-                if (MASKED) {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int e = slot(u, v);
-                        f2 base = FOLD ? bt[e] : bt[e] - lse2[u];   // FOLD: 2^-lse rides in dO and -delta
-                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                        f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
-                        s = bc::pfma(q[u].x[1], kk[v][1], s);
-                        const f2 p = bc::exp2_2(s);
-                        f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
-                        tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
-                        const f2 ds = p * tt;
-                        dq[u].x[0] = bc::pfma(ds, kk[v][0], dq[u].x[0]);
-                        dq[u].x[1] = bc::pfma(ds, kk[v][1], dq[u].x[1]);
-                        od[e] += ds;
-                    }
-                }
-#if MMNI_Q4_DSADD
-#pragma unroll
-                for (int e = 0; e < 9; ++e) {
-                    float* pe = reinterpret_cast<float*>(dp + (dcode(e) + DMIN - x) * EB);
-                    __hip_atomic_fetch_add(pe, od[e].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(pe + 1, od[e].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-#else
-#pragma unroll
-                for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (dcode(e) + DMIN - x) * EB) = od[e];
-                asm volatile("" ::: "memory");   // the next quad's entry reads stay behind these stores
-#endif
-#pragma unroll
-                for (int v = 0; v < 4; ++v)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) { kk[v][c] = nk[v][c]; vv[v][c] = nv[v][c]; }
-#pragma unroll
-                for (int e = 0; e < 9; ++e) bt[e] = nb[e];
-            }
-        }
-    }
-}
-
-// pass A, quad layout: 4 waves per workgroup, one head pair per workgroup, each wave one window at
-// a time with its own key records and private table-gradient image; no block barrier in the loop
-// (a wave reads only what it wrote; LDS runs a wave's accesses in order)
-__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
-void wattn_bwdA_q4_kernel(WAArgs a, float* part) {
-    using namespace q4;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    char* sm = reinterpret_cast<char*>(smem);
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const Work wk = work(NHG, wave);
-    float* tab = reinterpret_cast<float*>(sm + TAB);
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
-    float* dtf = reinterpret_cast<float*>(sm + DT);
-    for (int e = tid; e < WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
-    __syncthreads();
-    const bool lane_ok = lane < NB;
-    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
-    const int tb0 = base_token(beta), lcode = base_code(beta);
-    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
-    const int kvw = wave * KVB, dtw = DT + wave * TABB;
-    const int coff = wk.hp * 4;
-    const f2 qscale = bc::splat(a.scale * kLog2e);
-    for (int j = wk.j0;; j += wk.dj) {
-        const int w = wk.xcd + 8 * j;
-        if (w >= g.nwin) break;
-        Row q[4], dO[4], dq[4];
-        f2 lse2[4], ndl[4];
-        int rq[4] = {0, 0, 0, 0};
-        int64_t row[4] = {0, 0, 0, 0};
-        const bc::Regions reg = bc::window_regions(g, w);
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
-                row[u] = ti.row;
-                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
-                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
-                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
-                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
-                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
-                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
-                q[u].x[0] *= qscale;
-                q[u].x[1] *= qscale;
-                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
-                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
-                char* rec = sm + kvw + beta * REC + u * 32;   // key u of quad beta
-                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
-                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
-                dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
-            }
-        }
-        asm volatile("" ::: "memory");   // the records are written before the walk reads them
-        bool ok = true;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ok = ok && bc::fold_ok(lse2[u]);
-        const bool fold = __all(!lane_ok || ok);
-        if (lane_ok) {
-            if (fold) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const f2 e = bc::exp2_2(-lse2[u]);
-                    dO[u].x[0] *= e;
-                    dO[u].x[1] *= e;
-                    ndl[u] *= e;
-                }
-            }
-#define MMNI_Q4A(M, F) q4A_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw)
-            if (fold) {
-                if (reg.masked) MMNI_Q4A(true, true);
-                else MMNI_Q4A(false, true);
-            } else {
-                if (reg.masked) MMNI_Q4A(true, false);
-                else MMNI_Q4A(false, false);
-            }
-#undef MMNI_Q4A
-#pragma unroll
-            for (int u = 0; u < 4; ++u) bc::store_row_nat(a.dq + row[u] * a.qs + coff, dq[u], a.scale);
-        }
-        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
-    }
-    __syncthreads();
-    // this workgroup's partial row: its head pair's columns (waves 0..3 summed in order), zeros elsewhere
-    float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
-    for (int e = tid; e < TSZ * NHT; e += blockDim.x) {
-        const int r = e / NHT, c = e - r * NHT;
-        float v = 0.f;
-        if ((c >> 1) == wk.hp) {
-            const int o = r * 2 + (c & 1);
-            v = ((dtf[o] + dtf[TSZ * 2 + o]) + dtf[TSZ * 4 + o]) + dtf[TSZ * 6 + o];
-        }
-        prow[e] = v;
-    }
-}
-
 // ------------------------------------------------------------------------------------
 // merged backward, quad layout: pass A's walk (lane = query quad, key quads broadcast) also forms
 // the key side.  Per step a lane holds, for the 4 keys of the quad, its partial dk and dv over its
@@ -974,18 +429,7 @@ void wattn_bwdA_q4_kernel(WAArgs a, float* part) {
 // window, so those sums are final: no dk/dv accumulation, and p, ds are formed once per (query,
 // key) instead of once in each pass.  Deterministic (fixed lane tree, fixed row order).
 // ------------------------------------------------------------------------------------
-#ifndef MMNI_Q4M_UNROLL
-#define MMNI_Q4M_UNROLL 1   // unroll the merged walk's key loop
-#endif
-#ifndef MMNI_Q4M_PIPE
-#define MMNI_Q4M_PIPE 0     // issue the next key quad's records during the lane reduction
-#endif
 namespace q4 {
-// The spare lanes (54..63) of the merged walk run every step with zero dO, delta and q (so their
-// ds and partials are exactly 0) and read-modify-write table entries at this code: 6 is no
-// c_r + a * 3 TW + b * 3 TH (|a|, |b| <= 2) for any row-quad code c_r, so within one step their
-// entries never meet a real lane's, and they write back the values they read.  No branch.
-constexpr int kSpareCode = 6;
 __constant__ unsigned char kInvPermQ[NB] = {0, 1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 22, 23, 24, 25, 26, 27, 32, 33, 34, 28, 29, 30, 35, 36, 6, 7, 8, 9, 37, 38, 17, 18, 19, 20, 39, 40, 41, 21, 42, 43, 44, 45, 31, 46, 47, 48, 49, 50, 10, 51, 52, 53};
 
 template <int CTRL>
@@ -1048,11 +492,10 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
     const char* kv = sm + kvw;
     const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
     const int vsel = (lane >> 3) & 3;   // the key whose sum this lane ends with (l >> 1 = kind, v, c, h)
-    // MMNI_Q4M_PIPE: after a step's table stores, the next step's records and bias entries are
-    // issued and the step's lane reduction (pure VALU) runs while they are in flight.  The table
-    // base goes through an empty asm after the stores, so the compiler treats the next step's table
-    // reads as possibly aliasing them (other lanes' entries) and keeps them behind the stores; LDS
-    // executes a wave's accesses in order, so no wait is needed.
+    // The table image offset goes through an empty asm after each step's stores, so the compiler
+    // treats the next step's table reads as possibly aliasing them (other lanes' entries) and keeps
+    // them behind the stores; LDS executes a wave's accesses in order, so no wait is needed.  (Issuing
+    // the next step's records before the lane reduction measured no faster.)
     f2 kk[4][2], vv[4][2], bt[9], od[9];
     auto load = [&](const char* rec, const char* te) {
 #pragma unroll
@@ -1064,19 +507,14 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
         for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
     };
     int dto = dtw;   // this wave's table-gradient image (an LDS offset: the accesses stay ds_*)
-    if (MMNI_Q4M_PIPE) load(kv, sm + TAB + lane_e);
     for (int zr = 0; zr < 3; ++zr) {
         for (int yr = 0; yr < 3; ++yr) {
             const uint32_t trow = lane_e - (uint32_t)((zr * TW + yr * TH) * EB);
-            const int yn = yr + 1 < 3 ? yr + 1 : 0, zn = yr + 1 < 3 ? zr : zr + 1;
-            const bool last = zn == 3;   // the final row's prefetch re-reads itself (unused)
-            const uint32_t trown = last ? trow : lane_e - (uint32_t)((zn * TW + yn * TH) * EB);
             const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
-            const char* kvn = last ? kvr : kv + (zn * 3 + yn) * 6 * REC;
 #pragma unroll
             for (int x = 0; x < 6; ++x) {
-                // spare lanes skip the step (a divergent branch here measured spill-free; without it
-                // the compiler spilled ~800 VGPRs) and contribute zero partials
+                // spare lanes skip the step and contribute zero partials (as straight-line code for
+                // all lanes, with zero rows, the compiler spilled ~800 VGPRs; the branch does not)
                 f2 P[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) P[i] = bc::splat(0.f);
@@ -1085,7 +523,7 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
                     // this step's table-gradient entries (after the previous step's stores: see dto)
 #pragma unroll
                     for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (dcode(e) + DMIN - x) * EB);
-                    if (!MMNI_Q4M_PIPE) load(kvr + x * REC, sm + TAB + trow - x * EB);
+                    load(kvr + x * REC, sm + TAB + trow - x * EB);
                     int rk[4] = {0, 0, 0, 0};
                     if (MASKED) {
 #pragma unroll
@@ -1124,11 +562,6 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
                     for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (dcode(e) + DMIN - x) * EB) = od[e];
                 }
                 asm volatile("" : "+v"(dto));   // next reads: behind the stores above (see the top)
-                __builtin_amdgcn_sched_barrier(0);   // keep later steps' loads from being hoisted (registers)
-                if (MMNI_Q4M_PIPE) {
-                    if (x + 1 < 6) load(kvr + (x + 1) * REC, sm + TAB + trow - (x + 1) * EB);
-                    else load(kvn, sm + TAB + trown);
-                }
                 // all 64 lanes take part in the reduction (spare lanes contribute zeros)
                 const float sum = reduce32(P, lane);
                 // rows of key quad n = (zr, yr, x): held by the lane that owns query quad n
@@ -1159,8 +592,8 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
     for (int e = tid; e < WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
     __syncthreads();
     const bool lane_ok = lane < NB;
-    const int beta = lane_ok ? (int)kPermQ[lane] : 0;   // spare lanes run the walk on zero rows
-    const int tb0 = base_token(beta), lcode = lane_ok ? base_code(beta) : kSpareCode;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;   // spare lanes (54..63) only join the reductions
+    const int tb0 = base_token(beta), lcode = base_code(beta);
     const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
     const int kvw = wave * KVB, dtw = DT + wave * TABB;
     const int coff = wk.hp * 4;
@@ -1246,376 +679,6 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
     }
 }
 
-// ------------------------------------------------------------------------------------
-// pass B, quad layout: lane = key quad (4 keys), the wave walks the 54 query quads; query records
-// (q * scale * log2 e, dO [* 2^-lse], -delta [* 2^-lse], lse) broadcast from LDS; dk, dv in registers
-// ------------------------------------------------------------------------------------
-#ifndef MMNI_Q4B_UNROLL
-#define MMNI_Q4B_UNROLL 6
-#endif
-namespace q4 {
-constexpr int QREC = 192;                           // query-quad record: 4 x (q f4, dO f4, (-delta, lse) f4)
-constexpr int QRB = NB * QREC;                      // 10368 B per wave
-constexpr int TAB_B = WAVES * QRB;                  // bias table after the records (row bases >= 0)
-constexpr int LDS_B = TAB_B + TABB;                 // 52120 B: three workgroups per CU
-}  // namespace q4
-
-template <bool MASKED, bool FOLD>
-__device__ __forceinline__ void q4B_loop(const Row (&kr)[4], const Row (&vr)[4], Row (&dk)[4], Row (&dv)[4],
-                                         int lcode, const int (&rk)[4], const bc::Regions& reg, const char* sm,
-                                         int qrw) {
-    using namespace q4;
-    const char* qr = sm + qrw;
-    // entry of (query quad m, row u; key row v) = code(m) - code(beta) + OFF + D(u, v); per query
-    // row (zr, yr) one base, immediates (D + DMIN + x) * EB per query x
-    const uint32_t lane_e = (uint32_t)((OFF - lcode - DMIN) * EB);
-    for (int zr = 0; zr < 3; ++zr) {
-        for (int yr = 0; yr < 3; ++yr) {
-            const char* tp = sm + TAB_B + (lane_e + (uint32_t)((zr * TW + yr * TH) * EB));
-            const char* qrr = qr + (zr * 3 + yr) * 6 * QREC;
-#if MMNI_Q4B_UNROLL == 1
-#pragma unroll 1
-#elif MMNI_Q4B_UNROLL == 2
-#pragma unroll 2
-#elif MMNI_Q4B_UNROLL == 3
-#pragma unroll 3
-#else
-#pragma unroll
-#endif
-            for (int x = 0; x < 6; ++x) {
-                const char* rec = qrr + x * QREC;
-                f2 bt[9];
-#pragma unroll
-                for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(tp + (dcode(e) + DMIN + x) * EB);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {       // query row u of the quad: record (q, dO, -delta, lse)
-                    f2 qq[2], gg[2], nd, ls;
-                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48), qq[0], qq[1]);
-                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48 + 16), gg[0], gg[1]);
-                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 48 + 32), nd, ls);
-                    int rq = 0;
-                    if (MASKED) rq = bc::region_code(reg, zr + 3 * (u >> 1), yr + 3 * (u & 1), x);
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {   // the lane's key row v
-                        const int e = slot(u, v);
-                        f2 base = FOLD ? bt[e] : bt[e] - ls;
-                        if (MASKED) base += bc::splat(rq == rk[v] ? 0.f : kMask2);
-                        f2 s = bc::pfma(qq[0], kr[v].x[0], base);
-                        s = bc::pfma(qq[1], kr[v].x[1], s);
-                        const f2 p = bc::exp2_2(s);
-                        f2 tt = bc::pfma(gg[0], vr[v].x[0], nd);
-                        tt = bc::pfma(gg[1], vr[v].x[1], tt);
-                        const f2 dsv = p * tt;
-                        dv[v].x[0] = bc::pfma(p, gg[0], dv[v].x[0]);
-                        dv[v].x[1] = bc::pfma(p, gg[1], dv[v].x[1]);
-                        dk[v].x[0] = bc::pfma(dsv, qq[0], dk[v].x[0]);
-                        dk[v].x[1] = bc::pfma(dsv, qq[1], dk[v].x[1]);
-                    }
-                }
-            }
-        }
-    }
-}
-
-#ifndef MMNI_Q4B_WPE
-#define MMNI_Q4B_WPE 2   // waves per SIMD of the quad pass B (3: 168 VGPRs, spills; measured slower)
-#endif
-__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(MMNI_Q4B_WPE)))
-void wattn_bwdB_q4_kernel(WAArgs a) {
-    using namespace q4;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    char* sm = reinterpret_cast<char*>(smem);
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const Work wk = work(NHG, wave);
-    float* tab = reinterpret_cast<float*>(sm + TAB_B);
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
-    __syncthreads();
-    const bool lane_ok = lane < NB;
-    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
-    const int tb0 = base_token(beta), lcode = base_code(beta);
-    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
-    const int qrw = wave * QRB;
-    const int coff = wk.hp * 4;
-    const float qs2 = a.scale * kLog2e;
-    for (int j = wk.j0;; j += wk.dj) {
-        const int w = wk.xcd + 8 * j;
-        if (w >= g.nwin) break;
-        Row kr[4], vr[4], dk[4], dv[4];
-        int rk[4] = {0, 0, 0, 0};
-        int64_t row[4] = {0, 0, 0, 0};
-        f2 l2[4];
-        const bc::Regions reg = bc::window_regions(g, w);
-        bool ok = true;
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
-                row[u] = ti.row;
-                rk[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
-                l2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
-                ok = ok && bc::fold_ok(l2[u]);
-            }
-        }
-        // the lanes' rows are the whole window: the fold is decided per wave = per window
-        const bool fold = __all(!lane_ok || ok);
-        if (lane_ok) {
-            char* rec = sm + qrw + beta * QREC;   // query quad beta
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                kr[u] = bc::load_row_pk(a.k + row[u] * a.ks + coff);
-                vr[u] = bc::load_row_pk(a.v + row[u] * a.vs + coff);
-                dk[u].x[0] = dk[u].x[1] = dv[u].x[0] = dv[u].x[1] = bc::splat(0.f);
-                const float4 qv = *reinterpret_cast<const float4*>(a.q + row[u] * a.qs + coff);
-                const float4 gv = *reinterpret_cast<const float4*>(a.dout + row[u] * a.os + coff);
-                const float4 ov = *reinterpret_cast<const float4*>(a.o + row[u] * a.os + coff);
-                const f2 e = fold ? bc::exp2_2(-l2[u]) : bc::splat(1.f);
-                const float d0 = ov.x * gv.x + ov.y * gv.y, d1 = ov.z * gv.z + ov.w * gv.w;
-                *reinterpret_cast<bc::f4*>(rec + u * 48) = (bc::f4){qv.x * qs2, qv.z * qs2, qv.y * qs2, qv.w * qs2};
-                *reinterpret_cast<bc::f4*>(rec + u * 48 + 16) =
-                    (bc::f4){gv.x * e.x, gv.z * e.y, gv.y * e.x, gv.w * e.y};
-                *reinterpret_cast<bc::f4*>(rec + u * 48 + 32) = (bc::f4){-d0 * e.x, -d1 * e.y, l2[u].x, l2[u].y};
-            }
-        }
-        asm volatile("" ::: "memory");   // the records are written before the walk reads them
-        if (lane_ok) {
-            if (fold) {
-                if (reg.masked) q4B_loop<true, true>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
-                else q4B_loop<false, true>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
-            } else {
-                if (reg.masked) q4B_loop<true, false>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
-                else q4B_loop<false, false>(kr, vr, dk, dv, lcode, rk, reg, sm, qrw);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                bc::store_row_nat(a.dv + row[u] * a.vs + coff, dv[u], 1.0f);
-                bc::store_row_nat(a.dk + row[u] * a.ks + coff, dk[u], kLn2);   // staged q2 = q * scale * log2e
-            }
-        }
-        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// forward, quad layout: lane = query quad, key-quad records (k, v) broadcast as in pass A; online
-// softmax as wattn_fwd_bc_kernel (bounded waves: no reference; others: lazy reference)
-// ------------------------------------------------------------------------------------
-template <bool MASKED, bool BOUNDED>
-__device__ __forceinline__ void q4F_loop(const Row (&q)[4], f2 (&m)[4], f2 (&l)[4], Row (&o)[4], int lcode,
-                                         const int (&rq)[4], const bc::Regions& reg, const char* sm, int kvw) {
-    using namespace q4;
-    const char* kv = sm + kvw;
-    const char* tb = sm + TAB;
-    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
-    f2 kk[4][2], vv[4][2], bt[9];
-    auto fetch = [&](const char* rec, const char* te) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), kk[v][0], kk[v][1]);
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), vv[v][0], vv[v][1]);
-        }
-#pragma unroll
-        for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
-    };
-    if (BOUNDED) {
-        m[0] = m[1] = m[2] = m[3] = bc::splat(0.f);
-    } else {   // the reference: each row's exact maximum over key quad 0
-        fetch(kv, tb + lane_e);
-        int rk[4] = {0, 0, 0, 0};
-        if (MASKED) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, 3 * (v >> 1), 3 * (v & 1), 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            f2 mx = bc::splat(-INFINITY);
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                f2 base = bt[slot(u, v)];
-                if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
-                s = bc::pfma(q[u].x[1], kk[v][1], s);
-                mx = (f2){fmaxf(mx.x, s.x), fmaxf(mx.y, s.y)};
-            }
-            m[u] = mx;
-        }
-    }
-    for (int zr = 0; zr < 3; ++zr) {
-        for (int yr = 0; yr < 3; ++yr) {
-            const char* tp = tb + (lane_e - (uint32_t)((zr * TW + yr * TH) * EB));
-            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
-#pragma unroll
-            for (int x = 0; x < 6; ++x) {
-                fetch(kvr + x * REC, tp - x * EB);
-                int rk[4] = {0, 0, 0, 0};
-                if (MASKED) {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
-                }
-                if (BOUNDED) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            f2 base = bt[slot(u, v)];
-                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                            f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
-                            s = bc::pfma(q[u].x[1], kk[v][1], s);
-                            const f2 p = bc::exp2_2(s);
-                            l[u] += p;
-                            o[u].x[0] = bc::pfma(p, vv[v][0], o[u].x[0]);
-                            o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
-                        }
-                    }
-                    // no branch in the step: keep the compiler from hoisting the next reads (spills)
-                    __builtin_amdgcn_sched_barrier(0);
-                } else {
-                    f2 s[4][4];
-                    float smax = -INFINITY;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            f2 base = bt[slot(u, v)] - m[u];
-                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                            f2 sv = bc::pfma(q[u].x[0], kk[v][0], base);
-                            s[u][v] = bc::pfma(q[u].x[1], kk[v][1], sv);
-                            smax = fmaxf(smax, fmaxf(s[u][v].x, s[u][v].y));
-                        }
-                    }
-                    if (__any(smax > kLazy)) {   // rare: raise the reference of the rows that need it
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            f2 up = bc::splat(0.f);
-#pragma unroll
-                            for (int v = 0; v < 4; ++v) up = (f2){fmaxf(up.x, s[u][v].x), fmaxf(up.y, s[u][v].y)};
-                            const f2 alpha = bc::exp2_2(-up);
-                            l[u] *= alpha;
-                            o[u].x[0] *= alpha;
-                            o[u].x[1] *= alpha;
-                            m[u] += up;
-#pragma unroll
-                            for (int v = 0; v < 4; ++v) s[u][v] -= up;
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            const f2 p = bc::exp2_2(s[u][v]);
-                            l[u] += p;
-                            o[u].x[0] = bc::pfma(p, vv[v][0], o[u].x[0]);
-                            o[u].x[1] = bc::pfma(p, vv[v][1], o[u].x[1]);
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(3)))
-void wattn_fwd_q4_kernel(WAArgs a) {
-    using namespace q4;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    char* sm = reinterpret_cast<char*>(smem);
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const Work wk = work(NHG, wave);
-    float* tab = reinterpret_cast<float*>(sm + TAB);
-    float tabs = 0.f;   // this thread's entries all belong to head tid & 1 (the stride is even)
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
-        const float x = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
-        tab[e] = x;
-        tabs = fmaxf(tabs, fabsf(x));
-    }
-    for (int off = 2; off < 64; off <<= 1) tabs = fmaxf(tabs, __shfl_xor(tabs, off));
-    float* red = reinterpret_cast<float*>(sm + LDS_F);   // [WAVES][2] max |bias| per head
-    if (lane < 2) red[wave * 2 + lane] = tabs;
-    __syncthreads();
-    f2 tmax = bc::splat(0.f);
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) tmax = (f2){fmaxf(tmax.x, red[2 * i]), fmaxf(tmax.y, red[2 * i + 1])};
-    const bool lane_ok = lane < NB;
-    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
-    const int tb0 = base_token(beta), lcode = base_code(beta);
-    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
-    const int kvw = wave * KVB;
-    const int coff = wk.hp * 4;
-    const f2 qscale = bc::splat(a.scale * kLog2e);
-    float vabs = 0.f;
-    for (int j = wk.j0;; j += wk.dj) {
-        const int w = wk.xcd + 8 * j;
-        if (w >= g.nwin) break;
-        Row q[4], o[4];
-        f2 m[4], l[4];
-        int rq[4] = {0, 0, 0, 0};
-        int64_t row[4] = {0, 0, 0, 0};
-        const bc::Regions reg = bc::window_regions(g, w);
-        f2 kn = bc::splat(0.f);   // max |k|^2 per head over the lane's keys
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
-                row[u] = ti.row;
-                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
-                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
-                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
-                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
-                q[u].x[0] *= qscale;
-                q[u].x[1] *= qscale;
-                kn = (f2){fmaxf(kn.x, kr.x * kr.x + kr.y * kr.y), fmaxf(kn.y, kr.z * kr.z + kr.w * kr.w)};
-                vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
-                char* rec = sm + kvw + beta * REC + u * 32;
-                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
-                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
-                l[u] = bc::splat(0.f);
-                o[u].x[0] = o[u].x[1] = bc::splat(0.f);
-            }
-        }
-        asm volatile("" ::: "memory");   // the records are written before the walk reads them
-        for (int off = 1; off < 64; off <<= 1)
-            kn = (f2){fmaxf(kn.x, __shfl_xor(kn.x, off)), fmaxf(kn.y, __shfl_xor(kn.y, off))};
-        bool rows_ok = true;
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const f2 qn = bc::pfma(q[u].x[0], q[u].x[0], q[u].x[1] * q[u].x[1]);
-                const f2 qk = qn * kn;
-                rows_ok = rows_ok && __builtin_sqrtf(qk.x) + tmax.x <= kFwdBound &&
-                          __builtin_sqrtf(qk.y) + tmax.y <= kFwdBound;
-            }
-        }
-        const bool bounded = __all(rows_ok);
-        if (lane_ok) {
-            if (bounded) {
-                if (reg.masked) q4F_loop<true, true>(q, m, l, o, lcode, rq, reg, sm, kvw);
-                else q4F_loop<false, true>(q, m, l, o, lcode, rq, reg, sm, kvw);
-            } else {
-                if (reg.masked) q4F_loop<true, false>(q, m, l, o, lcode, rq, reg, sm, kvw);
-                else q4F_loop<false, false>(q, m, l, o, lcode, rq, reg, sm, kvw);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
-                Row r;
-                r.x[0] = o[u].x[0] * inv;
-                r.x[1] = o[u].x[1] * inv;
-                bc::store_row_nat(a.out + row[u] * a.os + coff, r, 1.0f);
-                a.lse[row[u] * NHT + 2 * wk.hp] = (m[u].x + fast_log2(l[u].x)) * kLn2;
-                a.lse[row[u] * NHT + 2 * wk.hp + 1] = (m[u].y + fast_log2(l[u].y)) * kLn2;
-            }
-        }
-        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
-    }
-    if (a.vmax != nullptr) {
-        for (int off = 32; off > 0; off >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, off));
-        if (lane == 0) atomicMax(a.vmax, __float_as_uint(vabs));
-    }
-}
-
 __global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < n) dtable[e] += src[e];
@@ -1631,8 +694,6 @@ bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind) {
     return g.wd == 6 && g.wh == 6 && g.ww == 6;
 }
 
-static size_t bcA_lds() { return (size_t)bc::align4(bc::Win<6, 6, 6>::TSZ * 6) * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8; }
-static size_t bcB_lds() { return (size_t)bc::align4(bc::Win<6, 6, 6>::TSZ * 2) * 4 + (size_t)12 * bc::Win<6, 6, 6>::H * 8; }
 
 // persistent grid: resident workgroups per CU from the LDS footprint and the register budget
 // (waves_per_eu of the kernel: 2-wave workgroups, 4 SIMDs), a multiple of 8 * NHG
@@ -1645,36 +706,17 @@ static int bc_blocks(size_t lds, int NHG, int waves_per_eu) {
     return grid < 8 * NHG ? 8 * NHG : grid;
 }
 
-#ifndef MMNI_BWDA_Q4
-#define MMNI_BWDA_Q4 1   // pass A in the quad layout (0: the row-pair kernel)
-#endif
-
-#ifndef MMNI_BWDB_Q4
-#define MMNI_BWDB_Q4 1   // pass B in the quad layout
-#endif
-#ifndef MMNI_FWD_Q4
-#define MMNI_FWD_Q4 0    // forward in the quad layout (measured 5% slower than the row-pair kernel)
-#endif
-
-// quad kernels: per_cu resident 4-wave workgroups per CU (pass A: 2 by LDS; pass B and the
-// forward: 3 by registers), a multiple of 8 with every head pair served
+// merged backward: per_cu resident 4-wave workgroups per CU (2 by LDS), a multiple of 8 with every
+// head pair served
 static int q4_blocks(int per_cu, int NHG) {
     int grid = per_cu * kNumCU;
     grid -= grid % 8;
     return grid < 8 * NHG ? 8 * NHG : grid;
 }
 
-#ifndef MMNI_BWD_MERGED
-#define MMNI_BWD_MERGED 1   // one merged quad kernel (dq, dk, dv, table) instead of passes A and B
-#endif
-
-static int bwdA_grid(int NHG) {
-    return (MMNI_BWDA_Q4 || MMNI_BWD_MERGED) ? q4_blocks(2, NHG) : bc_blocks(bcA_lds(), NHG, 2);
-}
-
 size_t wattn_bc_workspace_bytes(const WGeom& g, int heads) {
-    const int gridA = bwdA_grid(heads / 2);
-    return ((size_t)gridA + 1) * g.Tsz * heads * sizeof(float);
+    const int grid = q4_blocks(2, heads / 2);
+    return ((size_t)grid + 1) * g.Tsz * heads * sizeof(float);
 }
 
 static int set_lds_limit(const void* fn, size_t bytes) {
@@ -1695,12 +737,6 @@ int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_fwd (broadcast): compiled for 6^3 windows");
     const int NHG = heads / 2;
     a.hsplit = NHG;
-    if (MMNI_FWD_Q4) {
-        const size_t lds = (size_t)q4::LDS_F + 8 * sizeof(float);
-        const int grid = q4_blocks(3, NHG);
-        wattn_fwd_q4_kernel<<<grid, q4::WAVES * 64, lds, s>>>(a);
-        return launch_status("wattn_fwd_q4");
-    }
     const size_t lds = bcF_lds();
     const int grid = bc_blocks(lds, NHG, 4);
     int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_fwd_bc_kernel<6, 6, 6>), lds);
@@ -1715,35 +751,16 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_bwd (broadcast): compiled for 6^3 windows");
     const int NHG = heads / 2;
     a.hsplit = NHG;
-    const size_t ldsA = bcA_lds(), ldsB = bcB_lds();
-    const int gridA = bwdA_grid(NHG), gridB = MMNI_BWDB_Q4 ? q4_blocks(MMNI_Q4B_WPE, NHG) : bc_blocks(ldsB, NHG, 3);
-    const void* kA = MMNI_BWDA_Q4 ? reinterpret_cast<const void*>(&wattn_bwdA_q4_kernel)
-                                  : reinterpret_cast<const void*>(&wattn_bwdA_bc_kernel<6, 6, 6>);
-    const void* kB = reinterpret_cast<const void*>(&wattn_bwdB_bc_kernel<6, 6, 6>);
-    int rc = set_lds_limit(kA, MMNI_BWDA_Q4 ? (size_t)q4::LDS_A : ldsA);
-    if (rc) return rc;
-    rc = MMNI_BWDB_Q4 ? 0 : set_lds_limit(kB, ldsB);
+    const int grid = q4_blocks(2, NHG);
+    int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_bwd_q4m_kernel), q4::LDS_A);
     if (rc) return rc;
     const int ncol = g.Tsz * heads;
-    float* part = static_cast<float*>(workspace);          // [gridA][Tsz * heads]
-    float* sum = part + (size_t)gridA * ncol;              // [Tsz * heads]
-    if (MMNI_BWD_MERGED) {
-        rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_bwd_q4m_kernel), q4::LDS_A);
-        if (rc) return rc;
-        wattn_bwd_q4m_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
-        rc = launch_status("wattn_bwd_q4m");
-        if (rc) return rc;
-    } else {
-        if (MMNI_BWDA_Q4) wattn_bwdA_q4_kernel<<<gridA, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
-        else wattn_bwdA_bc_kernel<6, 6, 6><<<gridA, bc::kThreads, ldsA, s>>>(a, part);
-        rc = launch_status("wattn_bwdA_bc");
-        if (rc) return rc;
-        if (MMNI_BWDB_Q4) wattn_bwdB_q4_kernel<<<gridB, q4::WAVES * 64, q4::LDS_B, s>>>(a);
-        else wattn_bwdB_bc_kernel<6, 6, 6><<<gridB, bc::kThreads, ldsB, s>>>(a);
-        rc = launch_status("wattn_bwdB_bc");
-        if (rc) return rc;
-    }
-    column_sum(part, gridA, ncol, sum, ncol, nullptr, s);
+    float* part = static_cast<float*>(workspace);          // [grid][Tsz * heads]
+    float* sum = part + (size_t)grid * ncol;               // [Tsz * heads]
+    wattn_bwd_q4m_kernel<<<grid, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
+    rc = launch_status("wattn_bwd_q4m");
+    if (rc) return rc;
+    column_sum(part, grid, ncol, sum, ncol, nullptr, s);
     rc = launch_status("wattn_bwd_dtable_sum");
     if (rc) return rc;
     wattn_dtable_add_kernel<<<(ncol + 255) / 256, 256, 0, s>>>(sum, dtable, ncol);

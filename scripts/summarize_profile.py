@@ -26,8 +26,8 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk2?_kernel<(\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
-    m = re.search(r"mmni::wattn_bwd[AB]_bc_kernel<6, 6, 6>", name)   # kind 0, C = 12, 6^3 windows
-    if m:   # the row-broadcast backward: pass A + pass B (+ the table-gradient column sum) = one call
+    m = re.search(r"mmni::wattn_bwd[AB]_bc_kernel<6, 6, 6>|mmni::wattn_bwd[AB]_q4_kernel|mmni::wattn_bwd_q4m_kernel", name)
+    if m:   # kind 0, C = 12, 6^3 windows: the merged backward (older rounds: passes A + B) = one call
         return "wattn_bwd_k0_C12"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
     if m:
