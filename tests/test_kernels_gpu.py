@@ -69,6 +69,10 @@ WATTN = [
     (0, 12, 6, 1, (12, 24, 6), (6, 6, 6), (3, 3, 3), False),
     (0, 12, 6, 1, (18, 18, 18), (6, 6, 6), (3, 3, 3), False),   # interior (mask-free) windows
     (0, 12, 6, 2, (18, 12, 6), (6, 6, 6), (3, 3, 3), True),
+    # 6^3 kind-0 head pairs (merged quad backward) at 1, 2 and 4 head pairs per window
+    (0, 4, 2, 1, (12, 12, 12), (6, 6, 6), (3, 3, 3), False),
+    (0, 8, 4, 2, (6, 12, 6), (6, 6, 6), (3, 3, 3), True),
+    (0, 16, 8, 1, (12, 6, 12), (6, 6, 6), (0, 0, 0), False),
 ]
 
 
