@@ -3,8 +3,11 @@
 // :213-246, and the autograd backward of both).  Head pairs are packed into f2 lanes of
 // v_pk_fma_f32 (head 0, head 1), so a wave works on one head pair of one window at a time.
 //
-//   forward   wattn_fwd_bc_kernel   lane = query pair (t, t + N/2); the wave walks the keys in
-//                                   lock step, each key record an LDS broadcast read; online softmax
+//   forward   wattn_fwd_bcs_kernel  lane = query pair (t, t + N/2); the wave walks the keys in
+//                                   lock step, each key record an LDS broadcast read; online softmax;
+//                                   a 4-wave workgroup streams the query pairs of a list of windows
+//                                   (all lanes busy).  wattn_fwd_bc_kernel: one (window, head pair)
+//                                   per 2-wave workgroup (108 of 128 lanes)
 //   backward  wattn_bwd_q4m_kernel  lane = query quad (y + 3, z + 3 partners); the wave walks the
 //                                   54 key quads; per step p and ds of 16 (query, key) pairs give
 //                                   dq (registers), the bias-table gradient (private LDS image) and
@@ -679,6 +682,150 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// forward with streaming lanes.  A (window, head pair) has 108 query pairs, so the two-wave
+// workgroup above leaves 20 of its 128 lanes idle (84% lane use).  Here a 4-wave workgroup owns a
+// list of windows of one head pair and walks their query pairs as one sequence of slots, 256 per
+// round: every lane works, and a wave spans at most two windows (two broadcast addresses per
+// record read, their ring slots 16 bytes apart in bank order).  Each window's key records are
+// staged once into a 4-slot ring (a round touches at most 4 windows), with its max |k|^2 for the
+// bounded-step test.
+// ------------------------------------------------------------------------------------
+namespace fs {
+constexpr int WAVES = 4, RING = 4;
+constexpr int REC = 108 * 64;          // records of one window (pair t: keys t, t + 108)
+constexpr int SLOT = REC + 16;         // ring stride: consecutive slots 16 B apart modulo 128 B
+}  // namespace fs
+
+template <int WD, int WH, int WW>
+__global__ __launch_bounds__(fs::WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
+void wattn_fwd_bcs_kernel(WAArgs a) {
+    using Wn = bc::Win<WD, WH, WW>;
+    constexpr int H = Wn::H, TSZ = Wn::TSZ;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const WGeom& g = a.g;
+    const int NHG = a.hsplit, NHT = 2 * NHG;
+    float* tab_s = smem;                                        // [TSZ] f2: bias * log2e
+    char* ring = reinterpret_cast<char*>(tab_s + bc::align4(TSZ * 2));
+    float* red = reinterpret_cast<float*>(ring + fs::RING * fs::SLOT);   // [WAVES][2] max|bias|; [RING][2][2] max|k|^2
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // workgroup -> (XCD, head pair, window list): windows w = xcd + 8 (j0 + i), i < cnt
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = gridDim.x >> 3;
+    const int hp = slot % NHG, kb = slot / NHG, nblk = (nslots - hp + NHG - 1) / NHG;
+    const int nj = (g.nwin - xcd + 7) / 8, per = (nj + nblk - 1) / nblk, j0 = kb * per;
+    const int cnt = nj - j0 < 0 ? 0 : (nj - j0 < per ? nj - j0 : per);
+    float tabs = 0.f;
+    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
+        const float x = a.table[(e >> 1) * NHT + 2 * hp + (e & 1)] * kLog2e;
+        tab_s[e] = x;
+        tabs = fmaxf(tabs, fabsf(x));
+    }
+    for (int off = 2; off < 64; off <<= 1) tabs = fmaxf(tabs, __shfl_xor(tabs, off));
+    if (lane < 2) red[wave * 2 + lane] = tabs;
+    __syncthreads();
+    f2 tmax = bc::splat(0.f);
+#pragma unroll
+    for (int i = 0; i < fs::WAVES; ++i) tmax = (f2){fmaxf(tmax.x, red[2 * i]), fmaxf(tmax.y, red[2 * i + 1])};
+    float* kred = red + 2 * fs::WAVES;
+    const int coff = hp * 4;
+    const f2 qscale = bc::splat(a.scale * kLog2e);
+    float vabs = 0.f;
+    int staged = -1;
+    const int slots = cnt * H;
+    for (int s0 = 0; s0 < slots; s0 += fs::WAVES * 64) {
+        const int whi = (s0 + fs::WAVES * 64 - 1) / H < cnt - 1 ? (s0 + fs::WAVES * 64 - 1) / H : cnt - 1;
+        for (int wi = staged + 1; wi <= whi; ++wi) {   // stage the round's new windows
+            const int w = xcd + 8 * (j0 + wi);
+            char* rs = ring + (wi % fs::RING) * fs::SLOT;
+            f2 kn = bc::splat(0.f);
+            if (tid < H) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const TokenInfo ti = token_info(g, w, tid + u * H);
+                    const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
+                    const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
+                    kn = (f2){fmaxf(kn.x, kr.x * kr.x + kr.y * kr.y), fmaxf(kn.y, kr.z * kr.z + kr.w * kr.w)};
+                    vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
+                    f2* kv2 = reinterpret_cast<f2*>(rs) + tid * 8 + u * 4;
+                    kv2[0] = (f2){kr.x, kr.z};
+                    kv2[1] = (f2){kr.y, kr.w};
+                    kv2[2] = (f2){vr.x, vr.z};
+                    kv2[3] = (f2){vr.y, vr.w};
+                }
+            }
+            if (wave < 2) {   // the staging threads are waves 0 and 1
+                for (int off = 1; off < 64; off <<= 1)
+                    kn = (f2){fmaxf(kn.x, __shfl_xor(kn.x, off)), fmaxf(kn.y, __shfl_xor(kn.y, off))};
+                if (lane == 0) {
+                    kred[((wi % fs::RING) * 2 + wave) * 2] = kn.x;
+                    kred[((wi % fs::RING) * 2 + wave) * 2 + 1] = kn.y;
+                }
+            }
+        }
+        staged = whi > staged ? whi : staged;
+        __syncthreads();   // the round's records and bounds are in LDS
+        const int sl = s0 + tid;
+        const bool active = sl < slots;
+        const int wi = active ? sl / H : 0, pr = active ? sl - (sl / H) * H : 0;
+        const int w = xcd + 8 * (j0 + wi);
+        const int t = (int)bc::kPerm666[pr];
+        const int rslot = wi % fs::RING;
+        const bc::Regions reg = bc::window_regions(g, w);
+        Row q[2], o[2];
+        f2 m[2], l[2];
+        int cq = 0, rq[2] = {0, 0};
+        int64_t row[2] = {0, 0};
+        bool rows_ok = true;
+        if (active) {
+            const f2 kmax2 = (f2){fmaxf(kred[rslot * 4], kred[rslot * 4 + 2]), fmaxf(kred[rslot * 4 + 1], kred[rslot * 4 + 3])};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int tt = t + u * H;
+                const TokenInfo ti = token_info(g, w, tt);
+                row[u] = ti.row;
+                rq[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
+                if (u == 0) cq = ti.code + Wn::OFF;
+                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
+                q[u].x[0] *= qscale;
+                q[u].x[1] *= qscale;
+                l[u] = bc::splat(0.f);
+                o[u].x[0] = o[u].x[1] = bc::splat(0.f);
+                const f2 qn = bc::pfma(q[u].x[0], q[u].x[0], q[u].x[1] * q[u].x[1]);
+                const f2 qk = qn * kmax2;
+                rows_ok = rows_ok && __builtin_sqrtf(qk.x) + tmax.x <= kFwdBound &&
+                          __builtin_sqrtf(qk.y) + tmax.y <= kFwdBound;
+            }
+        }
+        const bool bounded = __all(rows_ok);
+        const bool masked = __any(active && reg.masked);   // the masked loop is exact for any window
+        const float* kv = reinterpret_cast<const float*>(ring + rslot * fs::SLOT);
+        if (active) {
+            if (bounded) {
+                if (masked) fwd_loop<WD, WH, WW, true, true>(q, m, l, o, cq, rq, reg, tab_s, kv);
+                else fwd_loop<WD, WH, WW, false, true>(q, m, l, o, cq, rq, reg, tab_s, kv);
+            } else {
+                if (masked) fwd_loop<WD, WH, WW, true, false>(q, m, l, o, cq, rq, reg, tab_s, kv);
+                else fwd_loop<WD, WH, WW, false, false>(q, m, l, o, cq, rq, reg, tab_s, kv);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
+                Row r;
+                r.x[0] = o[u].x[0] * inv;
+                r.x[1] = o[u].x[1] * inv;
+                bc::store_row_nat(a.out + row[u] * a.os + coff, r, 1.0f);
+                a.lse[row[u] * NHT + 2 * hp] = (m[u].x + fast_log2(l[u].x)) * kLn2;
+                a.lse[row[u] * NHT + 2 * hp + 1] = (m[u].y + fast_log2(l[u].y)) * kLn2;
+            }
+        }
+        __syncthreads();   // the round's record reads are done before the next round restages
+    }
+    if (a.vmax != nullptr) {
+        for (int off = 32; off > 0; off >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, off));
+        if (lane == 0) atomicMax(a.vmax, __float_as_uint(vabs));
+    }
+}
+
 __global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < n) dtable[e] += src[e];
@@ -731,12 +878,24 @@ static int set_lds_limit(const void* fn, size_t bytes) {
 
 static size_t bcF_lds() { return (size_t)bc::align4(bc::Win<6, 6, 6>::TSZ * 2) * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8 + 8 * 4; }
 
+#ifndef MMNI_FWD_STREAM
+#define MMNI_FWD_STREAM 1   // forward with streaming lanes (all 256 lanes of a workgroup busy)
+#endif
+
 int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     const WGeom& g = a.g;
     constexpr int kTsz666 = bc::Win<6, 6, 6>::TSZ;
     MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_fwd (broadcast): compiled for 6^3 windows");
     const int NHG = heads / 2;
     a.hsplit = NHG;
+    if (MMNI_FWD_STREAM) {
+        const size_t lds = (size_t)bc::align4(kTsz666 * 2) * 4 + (size_t)fs::RING * fs::SLOT +
+                           (size_t)(2 * fs::WAVES + 4 * fs::RING) * 4;
+        int per = (4 * kNumCU) / (8 * NHG);   // four 4-wave workgroups per CU (LDS, 128 VGPRs)
+        if (per < 1) per = 1;
+        wattn_fwd_bcs_kernel<6, 6, 6><<<8 * NHG * per, fs::WAVES * 64, lds, s>>>(a);
+        return launch_status("wattn_fwd_bcs");
+    }
     const size_t lds = bcF_lds();
     const int grid = bc_blocks(lds, NHG, 4);
     int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_fwd_bc_kernel<6, 6, 6>), lds);
