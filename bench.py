@@ -75,7 +75,9 @@ def parse():
     ap.add_argument("--size", type=int, default=None, help="volume side (voxels; default 96; c5: the fMRI side, 128)")
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1)")
+                    help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1); the "
+                         "default for the launch-bound configs c2 and c4 (a few hundred small kernels per step)")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture (c2 / c4 default to one at N = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-size", type=int, default=36)
     return ap.parse_args()
@@ -326,7 +328,7 @@ def main():
     else:
         kw = model_kwargs(args.size)
         model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
-    graph = args.graph and world == 1
+    graph = (args.graph or (args.config in ("c2", "c4") and not args.eager)) and world == 1
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank,
                               size_b=args.size * 3 // 4 if args.config == "c5" else None)
