@@ -50,8 +50,8 @@ struct TokArgs {
     const float* dy;     // bwd: (rows, N)
     const float* dres;   // bwd: (rows, C) residual gradient added to dx, or null
     float* dx;           // bwd: (rows, C)
-    float* partA;        // [waves][N*C + N]  dW | db
-    float* partB;        // [waves][2C]       dgamma | dbeta
+    float* partA;        // [waves][N*C + N (+ 2C)]  dW | db (| dgamma | dbeta)
+    float* partB;        // unused (dgamma | dbeta follow dW | db in partA's rows)
 };
 
 // ------------------------------------------------------------------------------------
@@ -244,9 +244,9 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
             }
         }
     }
-    // per-wave partials: A = [dW (N x C) | db (N)], B = [dgamma (C) | dbeta (C)]
-    float* pa = a.partA + wave * (N * C + N);
-    float* pb = a.partB + wave * (2 * C);
+    // per-wave partial row: [dW (N x C) | db (N) | dgamma (C) | dbeta (C)] (one column sum)
+    float* pa = a.partA + wave * (N * C + N + 2 * C);
+    float* pb = pa + (N * C + N);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
 #pragma unroll
@@ -384,7 +384,6 @@ extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const
         static const int wv = waves_of(&blk::ln_linear_bwd_kernel<NN, blk::llb_u(NN)>);                      \
         waves = wv < kNumCU * 8 * 4 ? wv : kNumCU * 8 * 4;                                           \
         a.partA = reinterpret_cast<float*>(workspace);                                              \
-        a.partB = a.partA + (size_t)waves * (N * C + N);                                            \
         blk::ln_linear_bwd_kernel<NN, blk::llb_u(NN)><<<waves / 4, 256, 0, s>>>(a);                           \
     }
     MMNI_LLB(12) MMNI_LLB(24) MMNI_LLB(36)
@@ -392,8 +391,17 @@ extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const
     (void)tiles;
     rc = launch_status("ln_linear_bwd");
     if (rc) return rc;
-    column_sum(a.partA, waves, N * C + N, dw, N * C, db, s);
-    column_sum(a.partB, waves, 2 * C, dgamma, C, dbeta, s);
+    ColSegs segs{};
+    segs.n = 4;
+    segs.end[0] = N * C;
+    segs.end[1] = N * C + N;
+    segs.end[2] = N * C + N + C;
+    segs.end[3] = N * C + N + 2 * C;
+    segs.dst[0] = dw;
+    segs.dst[1] = db;
+    segs.dst[2] = dgamma;
+    segs.dst[3] = dbeta;
+    column_sum_segs(a.partA, waves, N * C + N + 2 * C, segs, s);
     return launch_status("ln_linear_bwd_colsum");
 }
 

@@ -398,8 +398,10 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
         }
     }
     // per-wave partial rows: A = [dW1 (H x C) | db1 (H)], B = [dW2 (C x H) | db2 (C)]
-    float* pa = a.partA + wave * (H * C + H);
-    float* pb = a.partB + wave * (C * H + C);
+    // one partial row per wave: [dW1 | db1 | dW2 | db2 (| dgamma | dbeta)] (one column sum)
+    constexpr int RW = H * C + H + C * H + C + (LN ? 2 * C : 0);
+    float* pa = a.partA + wave * RW;
+    float* pb = pa + (H * C + H);
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) {
 #pragma unroll
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
     db2 += __shfl_xor(db2, 32);
     if (lg == 0 && li < C) pb[C * H + li] = db2;
     if constexpr (LN) {
-        float* pc = a.partC + wave * (2 * C);
+        float* pc = pb + (C * H + C);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float u = dgm[i], v = dbt[i];
@@ -511,15 +513,18 @@ template <bool LN>
 static int mlp_bwd_launch(const mmni_mlp_desc* d, mlpk::MlpArgs& a, float* dw1, float* db1, float* dw2, float* db2,
                           float* dgamma, float* dbeta, void* workspace, hipStream_t s) {
     const int C = d->C, H = d->H, waves = mlp_bwd_waves<LN>();
-    a.partA = reinterpret_cast<float*>(workspace);
-    a.partB = a.partA + (size_t)waves * (H * C + H);
-    a.partC = a.partB + (size_t)waves * (C * H + C);
+    a.partA = reinterpret_cast<float*>(workspace);   // [waves][dW1 | db1 | dW2 | db2 (| dgamma | dbeta)]
     mlpk::mlp_bwd_kernel<LN><<<waves / mlpk::kBwdWaves, 64 * mlpk::kBwdWaves, 0, s>>>(a);
     int rc = launch_status(LN ? "ln_mlp_bwd" : "mlp_bwd");
     if (rc) return rc;
-    column_sum(a.partA, waves, H * C + H, dw1, H * C, db1, s);
-    column_sum(a.partB, waves, C * H + C, dw2, C * H, db2, s);
-    if (LN) column_sum(a.partC, waves, 2 * C, dgamma, C, dbeta, s);
+    ColSegs segs{};
+    segs.n = LN ? 6 : 4;
+    const int e1 = H * C, e2 = e1 + H, e3 = e2 + C * H, e4 = e3 + C;
+    segs.end[0] = e1; segs.end[1] = e2; segs.end[2] = e3; segs.end[3] = e4;
+    segs.end[4] = e4 + C; segs.end[5] = e4 + 2 * C;
+    segs.dst[0] = dw1; segs.dst[1] = db1; segs.dst[2] = dw2; segs.dst[3] = db2;
+    segs.dst[4] = dgamma; segs.dst[5] = dbeta;
+    column_sum_segs(a.partA, waves, LN ? e4 + 2 * C : e4, segs, s);
     return launch_status("mlp_colsum");
 }
 

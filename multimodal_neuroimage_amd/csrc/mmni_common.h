@@ -40,5 +40,16 @@ constexpr int kNumCU = 256;
 // out[j] = sum_b part[b][j] over a (nparts, ncols) slab in a fixed order (deterministic); columns
 // j >= split go to out2[j - split] (tokenops.hip).
 void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s);
+// Column sums of one partial matrix into up to kMax destination segments: columns
+// [end[k-1], end[k]) go to dst[k] (end[-1] = 0; a null dst drops them), written or, with
+// accumulate, added.  Same fixed-order reduction as column_sum.
+struct ColSegs {
+    static constexpr int kMax = 6;
+    int n;
+    int end[kMax];
+    float* dst[kMax];
+    int accumulate;
+};
+void column_sum_segs(const float* part, int nparts, int ncols, const ColSegs& segs, hipStream_t s);
 
 }  // namespace mmni

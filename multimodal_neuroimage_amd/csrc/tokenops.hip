@@ -160,8 +160,7 @@ __global__ __launch_bounds__(1024) void column_sum_stage1_kernel(float* __restri
 }
 
 __global__ __launch_bounds__(256) void column_sum_stage2_kernel(const float* __restrict__ part, int nparts, int ncols,
-                                                                int rps, int nslices, float* __restrict__ out,
-                                                                int split, float* __restrict__ out2) {
+                                                                int rps, int nslices, ColSegs segs) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= ncols) return;
     // all slice loads issued before the (in-order, double) sum: one memory latency, not 2 x nslices
@@ -180,11 +179,22 @@ __global__ __launch_bounds__(256) void column_sum_stage2_kernel(const float* __r
             if (nparts - sl * rps > 1) t += (double)lo[sl];
         }
     }
-    if (j < split) out[j] = (float)t;
-    else if (out2) out2[j - split] = (float)t;
+    // column j -> segment k (columns [end[k-1], end[k]) go to dst[k]; a null dst drops them)
+    int k = 0, begin = 0;
+#pragma unroll
+    for (int i = 0; i < ColSegs::kMax - 1; ++i) {
+        if (i < segs.n - 1 && j >= segs.end[i]) {
+            k = i + 1;
+            begin = segs.end[i];
+        }
+    }
+    float* d = segs.dst[k];
+    if (d == nullptr) return;
+    if (segs.accumulate) d[j - begin] += (float)t;
+    else d[j - begin] = (float)t;
 }
 
-void column_sum(const float* part_c, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
+void column_sum_segs(const float* part_c, int nparts, int ncols, const ColSegs& segs, hipStream_t s) {
     float* part = const_cast<float*>(part_c);   // scratch: stage 1 leaves its sums in place
     const int want = kColSlices;                // row slices
     int rps = (nparts + want - 1) / want;
@@ -196,7 +206,17 @@ void column_sum(const float* part_c, int nparts, int ncols, float* out, int spli
         column_sum_stage1_kernel<32><<<dim3((ncols + 31) / 32, nslices), 1024, 0, s>>>(part, nparts, ncols, rps);
     else
         column_sum_stage1_kernel<64><<<dim3((ncols + 63) / 64, nslices), 1024, 0, s>>>(part, nparts, ncols, rps);
-    column_sum_stage2_kernel<<<(ncols + 255) / 256, 256, 0, s>>>(part, nparts, ncols, rps, nslices, out, split, out2);
+    column_sum_stage2_kernel<<<(ncols + 255) / 256, 256, 0, s>>>(part, nparts, ncols, rps, nslices, segs);
+}
+
+void column_sum(const float* part, int nparts, int ncols, float* out, int split, float* out2, hipStream_t s) {
+    ColSegs segs{};
+    segs.n = 2;
+    segs.end[0] = split;
+    segs.end[1] = ncols;
+    segs.dst[0] = out;
+    segs.dst[1] = out2;
+    column_sum_segs(part, nparts, ncols, segs, s);
 }
 
 using f4 = __attribute__((ext_vector_type(4))) float;

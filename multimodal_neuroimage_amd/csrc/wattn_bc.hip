@@ -826,10 +826,6 @@ void wattn_fwd_bcs_kernel(WAArgs a) {
     }
 }
 
-__global__ void wattn_dtable_add_kernel(const float* src, float* dtable, int n) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dtable[e] += src[e];
-}
 
 // ------------------------------------------------------------------------------------
 // host side
@@ -915,15 +911,16 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     if (rc) return rc;
     const int ncol = g.Tsz * heads;
     float* part = static_cast<float*>(workspace);          // [grid][Tsz * heads]
-    float* sum = part + (size_t)grid * ncol;               // [Tsz * heads]
     wattn_bwd_q4m_kernel<<<grid, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
     rc = launch_status("wattn_bwd_q4m");
     if (rc) return rc;
-    column_sum(part, grid, ncol, sum, ncol, nullptr, s);
-    rc = launch_status("wattn_bwd_dtable_sum");
-    if (rc) return rc;
-    wattn_dtable_add_kernel<<<(ncol + 255) / 256, 256, 0, s>>>(sum, dtable, ncol);
-    return launch_status("wattn_bwd_dtable_add");
+    ColSegs segs{};   // dtable += the fixed-order column sums of the workgroups' partial rows
+    segs.n = 1;
+    segs.end[0] = ncol;
+    segs.dst[0] = dtable;
+    segs.accumulate = 1;
+    column_sum_segs(part, grid, ncol, segs, s);
+    return launch_status("wattn_bwd_dtable_sum");
 }
 
 }  // namespace mmni
