@@ -258,6 +258,13 @@ int mmni_mlp_bwd(const mmni_mlp_desc* d, const float* x, const float* w1, const 
 int mmni_ln_mlp_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
                     const float* w1, const float* b1, const float* w2, const float* b2, int residual_x, float* y,
                     void* stream);
+/* mmni_ln_mlp_fwd plus the identity skip of the residual group that ends with this block
+ * (RSTB / CRSTB `residual_group(x) + x`, swinfusion_module.py:814,918-927):
+ * y = [x] + fc2(GELU(fc1(LN(x)))) + skip.  skip is (rows, C) contiguous, 16-byte aligned and must
+ * not alias y; its gradient is dy itself, so mmni_ln_mlp_bwd serves both forms. */
+int mmni_ln_mlp_skip_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
+                         const float* w1, const float* b1, const float* w2, const float* b2, int residual_x,
+                         const float* skip, float* y, void* stream);
 int mmni_ln_mlp_bwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
                     const float* w1, const float* b1, const float* w2, const float* dy, int residual_x, float* dx,
                     float* dgamma, float* dbeta, float* dw1, float* db1, float* dw2, float* db2, void* workspace,

@@ -94,6 +94,7 @@ SIGNATURES = {
     "mmni_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
     "mmni_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc)] + [_vp] * 12),
     "mmni_ln_mlp_fwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int, _vp, _vp]),
+    "mmni_ln_mlp_skip_fwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int, _vp, _vp, _vp]),
     "mmni_ln_mlp_bwd": (_c_int, [ctypes.POINTER(MlpDesc), _c_f] + [_vp] * 7 + [_c_int] + [_vp] * 9),
     "mmni_zscore_workspace_bytes": (ctypes.c_size_t, [_c_i64]),
     "mmni_zscore": (_c_int, [_c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp]),

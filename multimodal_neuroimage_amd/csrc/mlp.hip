@@ -76,6 +76,7 @@ struct MlpArgs {
     const float* w2;   // (C, H)
     const float* b2;   // (C)
     const float* res;  // (rows, C) contiguous, or null
+    const float* res2; // forward: a second addend (the residual group's skip), or null
     float* y;
     // LayerNorm prologue (LN kernels): x -> (x - mean) * rstd * gamma + beta over the C channels
     const float* gamma;
@@ -172,11 +173,12 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
     // the next tile's x and residual are loaded while this tile computes (one tile in flight per
     // wave otherwise leaves the chain load -> LN -> MFMA -> GELU -> MFMA exposed)
     float xn[CS] = {0.f, 0.f, 0.f};
-    f4 rn = (f4){0.f, 0.f, 0.f, 0.f};
+    f4 rn = (f4){0.f, 0.f, 0.f, 0.f}, sn = rn;
     auto fetch = [&](int64_t tile) {
         const int64_t t0 = tile * 16;
         io.load_fm(a.x, t0, xn);
         if (a.res != nullptr && io.row_ok(t0)) rn = *reinterpret_cast<const f4*>(a.res + (t0 + li) * C + 4 * lg);
+        if (a.res2 != nullptr && io.row_ok(t0)) sn = *reinterpret_cast<const f4*>(a.res2 + (t0 + li) * C + 4 * lg);
     };
     if (wave < tiles) fetch(wave);
     for (int64_t tile = wave; tile < tiles; tile += nwaves) {
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
         float xb[CS];
 #pragma unroll
         for (int s = 0; s < CS; ++s) xb[s] = xn[s];
-        const f4 rv = rn;
+        const f4 rv = rn, sv = sn;
         if (tile + nwaves < tiles) fetch(tile + nwaves);
         if constexpr (LN) {
             float mean, rstd;
@@ -196,6 +198,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
         const int64_t roff = (t0 + li) * C + 4 * lg;
         f4 acc = b2c;
         if (a.res != nullptr && ok) acc += rv;
+        if (a.res2 != nullptr && ok) acc += sv;
         // three independent accumulator chains (one per hidden tile), summed at the end
         f4 out[HT];
 #pragma unroll
@@ -488,19 +491,32 @@ extern "C" int mmni_mlp_fwd(const mmni_mlp_desc* d, const float* x, const float*
     return mlp_fwd_launch<false>(d, a, (hipStream_t)stream);
 }
 
-extern "C" int mmni_ln_mlp_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma,
-                               const float* beta, const float* w1, const float* b1, const float* w2, const float* b2,
-                               int residual_x, float* y, void* stream) {
+static int ln_mlp_fwd_impl(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma, const float* beta,
+                           const float* w1, const float* b1, const float* w2, const float* b2, int residual_x,
+                           const float* skip, float* y, void* stream) {
     int rc = mlp_check(d);
     if (rc) return rc;
     MMNI_ARG_CHECK(x && gamma && beta && w1 && w2 && y, "ln_mlp_fwd: null pointer");
-    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
-                   "ln_mlp_fwd: x / y must be 16-byte aligned");
+    MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(skip) % 16 == 0, "ln_mlp_fwd: x / skip / y must be 16-byte aligned");
     mlpk::MlpArgs a{};
     a.rows = d->rows;
     a.x = x; a.gamma = gamma; a.beta = beta; a.eps = eps;
-    a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.res = residual_x ? x : nullptr; a.y = y;
+    a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.res = residual_x ? x : nullptr; a.res2 = skip; a.y = y;
     return mlp_fwd_launch<true>(d, a, (hipStream_t)stream);
+}
+
+extern "C" int mmni_ln_mlp_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma,
+                               const float* beta, const float* w1, const float* b1, const float* w2, const float* b2,
+                               int residual_x, float* y, void* stream) {
+    return ln_mlp_fwd_impl(d, eps, x, gamma, beta, w1, b1, w2, b2, residual_x, nullptr, y, stream);
+}
+
+extern "C" int mmni_ln_mlp_skip_fwd(const mmni_mlp_desc* d, float eps, const float* x, const float* gamma,
+                                    const float* beta, const float* w1, const float* b1, const float* w2,
+                                    const float* b2, int residual_x, const float* skip, float* y, void* stream) {
+    MMNI_ARG_CHECK(skip != nullptr && skip != y, "ln_mlp_skip_fwd: skip must be a separate (rows, C) buffer");
+    return ln_mlp_fwd_impl(d, eps, x, gamma, beta, w1, b1, w2, b2, residual_x, skip, y, stream);
 }
 
 extern "C" size_t mmni_mlp_bwd_workspace_bytes(const mmni_mlp_desc* d) {

@@ -679,17 +679,24 @@ class _LnMlp(torch.autograd.Function):
     statistics never reach HBM; the backward adds the LN backward and the residual gradient."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, w1, b1, w2, b2, eps, residual_x):
+    def forward(ctx, x, gamma, beta, w1, b1, w2, b2, eps, residual_x, skip):
         H, C = w1.shape
         x2 = x.reshape(-1, C).contiguous()
         rows = x2.shape[0]
         y = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
         d = _mlp_desc(rows, C, H, C, C)
+        L = _lib.load()
         ev = KernelTimer.start()
-        check(_lib.load().mmni_ln_mlp_fwd(ctypes.byref(d), float(eps), ptr(x2), ptr(gamma), ptr(beta), ptr(w1), ptr(b1),
-                                          ptr(w2), ptr(b2), int(residual_x), ptr(y), stream_handle(x2.device)),
-              "mmni_ln_mlp_fwd")
-        KernelTimer.stop(f"ln_mlp_fwd_{C}x{H}", ev, 4.0 * rows * C * H, 4.0 * rows * C * 2)
+        if skip is None:
+            check(L.mmni_ln_mlp_fwd(ctypes.byref(d), float(eps), ptr(x2), ptr(gamma), ptr(beta), ptr(w1), ptr(b1),
+                                    ptr(w2), ptr(b2), int(residual_x), ptr(y), stream_handle(x2.device)),
+                  "mmni_ln_mlp_fwd")
+        else:
+            s2 = skip.reshape(-1, C).contiguous()
+            check(L.mmni_ln_mlp_skip_fwd(ctypes.byref(d), float(eps), ptr(x2), ptr(gamma), ptr(beta), ptr(w1),
+                                         ptr(b1), ptr(w2), ptr(b2), int(residual_x), ptr(s2), ptr(y),
+                                         stream_handle(x2.device)), "mmni_ln_mlp_skip_fwd")
+        KernelTimer.stop(f"ln_mlp_fwd_{C}x{H}", ev, 4.0 * rows * C * H, 4.0 * rows * C * (2 if skip is None else 3))
         ctx.save_for_backward(x2, gamma, beta, w1, b1, w2)
         ctx.has_b = (b1 is not None, b2 is not None)
         ctx.eps, ctx.residual_x, ctx.xshape = float(eps), bool(residual_x), x.shape
@@ -717,7 +724,7 @@ class _LnMlp(torch.autograd.Function):
                                 ptr(dw2), ptr(db2), ptr(ws), stream_handle(dev)), "mmni_ln_mlp_bwd")
         KernelTimer.stop(f"ln_mlp_bwd_{C}x{H}", ev, 10.0 * rows * C * H, 4.0 * rows * C * 3)
         return (dx.view(ctx.xshape), dgamma, dbeta, dw1, db1 if ctx.has_b[0] else None, dw2,
-                db2 if ctx.has_b[1] else None, None, None)
+                db2 if ctx.has_b[1] else None, None, None, dy if ctx.needs_input_grad[9] else None)
 
 
 def ln_mlp_ok(x, norm, mlp_mod):
@@ -729,15 +736,20 @@ def ln_mlp_ok(x, norm, mlp_mod):
             and bool(_lib.load().mmni_mlp_supported(C, H)))
 
 
-def ln_mlp(x, norm, mlp_mod, residual_x=True):
-    """[x +] mlp_mod(norm(x)) for an Mlp / Mlp_fusion module (fc1, act, fc2, drop), fused into one
-    kernel per direction when ln_mlp_ok; else LayerNorm + the MLP path."""
+def ln_mlp(x, norm, mlp_mod, residual_x=True, skip=None):
+    """[x +] mlp_mod(norm(x)) [+ skip] for an Mlp / Mlp_fusion module (fc1, act, fc2, drop), fused
+    into one kernel per direction when ln_mlp_ok; else LayerNorm + the MLP path.  skip is the
+    identity skip of a residual group ending with this block (swinfusion_module.py:814,918-927),
+    added in the same epilogue instead of by a separate full-size add."""
     require_device(x, what="ln_mlp")
+    if skip is not None and (skip.shape != x.shape or skip.dtype != torch.float32):
+        raise ValueError(f"ln_mlp: skip {tuple(skip.shape)} {skip.dtype} must match x {tuple(x.shape)} float32")
     if ln_mlp_ok(x, norm, mlp_mod):
         return _LnMlp.apply(x, norm.weight, norm.bias, mlp_mod.fc1.weight, mlp_mod.fc1.bias, mlp_mod.fc2.weight,
-                            mlp_mod.fc2.bias, float(norm.eps), residual_x)
-    return mlp(layer_norm(x, norm), mlp_mod.fc1, mlp_mod.fc2, mlp_mod.act, mlp_mod.drop,
-               residual=x if residual_x else None)
+                            mlp_mod.fc2.bias, float(norm.eps), residual_x, skip)
+    y = mlp(layer_norm(x, norm), mlp_mod.fc1, mlp_mod.fc2, mlp_mod.act, mlp_mod.drop,
+            residual=x if residual_x else None)
+    return y if skip is None else y + skip
 
 
 def mlp(x, fc1, fc2, act, drop, residual=None):

@@ -197,20 +197,24 @@ class SwinTransformerBlock_fusion(nn.Module):
         nd = len(x_size)
         return shift_mask_buffer(tuple(x_size), to_ntuple(self.window_size, nd), to_ntuple(self.shift_size, nd))
 
-    def forward(self, x, x_size):
+    def forward(self, x, x_size, skip=None):
+        """skip: the identity skip of the residual group this block ends (RSTB / CRSTB), added in
+        the MLP epilogue when the fused path runs (one full-size add less per group)."""
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
         if inactive(self.drop_path) and ln_linear_ok(x, self.norm1, self.attn.qkv):
             # norm1 + qkv in one kernel; the residual's gradient joins inside its backward
             qkv, xr = ln_linear(x, self.norm1, self.attn.qkv, passthrough=True)
             x = self.attn.attend(qkv.reshape(B * L, 3 * C), geom, residual=xr.reshape(B * L, C)).view(B, L, C)
-            return ln_mlp(x, self.norm2, self.mlp)   # x + mlp(norm2(x)), one kernel
+            return ln_mlp(x, self.norm2, self.mlp, skip=skip)   # x + mlp(norm2(x)) [+ skip], one kernel
         xn = layer_norm(x, self.norm1).reshape(B * L, C)
         if inactive(self.drop_path):   # residual adds fused into the proj / fc2 epilogues
             x = self.attn.forward_tokens(xn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
-            return self.mlp(layer_norm(x, self.norm2), residual=x)
-        x = x + self.drop_path(self.attn.forward_tokens(xn, geom).view(B, L, C))
-        return x + self.drop_path(self.mlp(layer_norm(x, self.norm2)))
+            x = self.mlp(layer_norm(x, self.norm2), residual=x)
+        else:
+            x = x + self.drop_path(self.attn.forward_tokens(xn, geom).view(B, L, C))
+            x = x + self.drop_path(self.mlp(layer_norm(x, self.norm2)))
+        return x if skip is None else x + skip
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads={self.num_heads}, "
@@ -252,7 +256,10 @@ class Cross_SwinTransformerBlock(nn.Module):
         nd = len(x_size)
         return shift_mask_buffer(tuple(x_size), to_ntuple(self.window_size, nd), to_ntuple(self.shift_size, nd))
 
-    def forward(self, x, y, x_size):
+    def forward(self, x, y, x_size, skip=None):
+        """skip: (skip_x, skip_y), the identity skips of the CRSTB inter-modal group this block
+        ends, added in the MLP epilogues on the fused path."""
+        sx, sy = skip if skip is not None else (None, None)
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
         if (inactive(self.drop_path_A) and inactive(self.drop_path_B)
@@ -266,21 +273,22 @@ class Cross_SwinTransformerBlock(nn.Module):
                                     residual=xr.reshape(B * L, C)).view(B, L, C)
             yb = self.attn_B.attend(qb.reshape(B * L, C), kvb.reshape(B * L, 2 * C), geom,
                                     residual=yr.reshape(B * L, C)).view(B, L, C)
-            return ln_mlp(xa, self.norm2_A, self.mlp_A), ln_mlp(yb, self.norm2_B, self.mlp_B)
+            return ln_mlp(xa, self.norm2_A, self.mlp_A, skip=sx), ln_mlp(yb, self.norm2_B, self.mlp_B, skip=sy)
         xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
         yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
         if inactive(self.drop_path_A) and inactive(self.drop_path_B):   # fused residual adds
             xa = self.attn_A.forward_tokens(xn, yn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
             yb = self.attn_B.forward_tokens(yn, xn, geom, residual=y.reshape(B * L, C)).view(B, L, C)
-            return (self.mlp_A(layer_norm(xa, self.norm2_A), residual=xa),
-                    self.mlp_B(layer_norm(yb, self.norm2_B), residual=yb))
-        a = self.attn_A.forward_tokens(xn, yn, geom).view(B, L, C)
-        b = self.attn_B.forward_tokens(yn, xn, geom).view(B, L, C)
-        x = x + self.drop_path_A(a)
-        x = x + self.drop_path_A(self.mlp_A(layer_norm(x, self.norm2_A)))
-        y = y + self.drop_path_B(b)
-        y = y + self.drop_path_B(self.mlp_B(layer_norm(y, self.norm2_B)))
-        return x, y
+            x = self.mlp_A(layer_norm(xa, self.norm2_A), residual=xa)
+            y = self.mlp_B(layer_norm(yb, self.norm2_B), residual=yb)
+        else:
+            a = self.attn_A.forward_tokens(xn, yn, geom).view(B, L, C)
+            b = self.attn_B.forward_tokens(yn, xn, geom).view(B, L, C)
+            x = x + self.drop_path_A(a)
+            x = x + self.drop_path_A(self.mlp_A(layer_norm(x, self.norm2_A)))
+            y = y + self.drop_path_B(b)
+            y = y + self.drop_path_B(self.mlp_B(layer_norm(y, self.norm2_B)))
+        return (x if sx is None else x + sx), (y if sy is None else y + sy)
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads={self.num_heads}, "
@@ -328,10 +336,17 @@ class BasicLayer_fusion(nn.Module):
             for i in range(depth)])
         self.downsample = downsample(input_resolution, dim=dim, norm_layer=norm_layer) if downsample else None
 
-    def forward(self, x, x_size):
-        for blk in self.blocks:
-            x = checkpoint.checkpoint(blk, x, x_size, use_reentrant=False) if self.use_checkpoint else blk(x, x_size)
-        return self.downsample(x) if self.downsample is not None else x
+    def forward(self, x, x_size, skip=None):
+        """skip: the enclosing residual group's identity skip (RSTB / CRSTB), handed to the last
+        block so it joins that block's MLP epilogue; added after the downsample when there is one."""
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            s = skip if (i == last and self.downsample is None) else None
+            x = checkpoint.checkpoint(blk, x, x_size, s, use_reentrant=False) if self.use_checkpoint else blk(x, x_size, s)
+        if self.downsample is not None:
+            x = self.downsample(x)
+            return x if skip is None else x + skip
+        return x if self.blocks or skip is None else x + skip
 
     def extra_repr(self):
         return f"dim={self.dim}, input_resolution={self.input_resolution}, depth={self.depth}"
@@ -358,14 +373,21 @@ class Cross_BasicLayer(nn.Module):
             for i in range(depth)])
         self.downsample = downsample(input_resolution, dim=dim, norm_layer=norm_layer) if downsample else None
 
-    def forward(self, x, y, x_size):
-        for blk in self.blocks:
+    def forward(self, x, y, x_size, skip=None):
+        """skip: (skip_x, skip_y) of the enclosing CRSTB, joined in the last block's MLP epilogues."""
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            s = skip if (i == last and self.downsample is None) else None
             if self.use_checkpoint:
-                x, y = checkpoint.checkpoint(blk, x, y, x_size, use_reentrant=False)
+                x, y = checkpoint.checkpoint(blk, x, y, x_size, s, use_reentrant=False)
             else:
-                x, y = blk(x, y, x_size)
+                x, y = blk(x, y, x_size, s)
         if self.downsample is not None:
             x, y = self.downsample(x), self.downsample(y)
+            if skip is not None:
+                x, y = x + skip[0], y + skip[1]
+        elif skip is not None and not self.blocks:
+            x, y = x + skip[0], y + skip[1]
         return x, y
 
     def extra_repr(self):
@@ -408,7 +430,8 @@ class RSTB(nn.Module):
                                           norm_layer=None)
 
     def forward(self, x, x_size):
-        return self.residual_group(x, x_size) + x
+        # residual_group(x) + x (:814), the "+ x" joined inside the group's last MLP epilogue
+        return self.residual_group(x, x_size, skip=x)
 
 
 class CRSTB(nn.Module):
@@ -447,10 +470,10 @@ class CRSTB(nn.Module):
                                           norm_layer=None)
 
     def forward(self, x, y, x_size):
-        x = self.residual_group_A(x, x_size) + x
-        y = self.residual_group_B(y, x_size) + y
-        xo, yo = self.residual_group(x, y, x_size)
-        return xo + x, yo + y
+        # the three identity skips (:918-927) joined inside each group's last MLP epilogue
+        x = self.residual_group_A(x, x_size, skip=x)
+        y = self.residual_group_B(y, x_size, skip=y)
+        return self.residual_group(x, y, x_size, skip=(x, y))
 
 
 class PatchEmbed_fusion(nn.Module):

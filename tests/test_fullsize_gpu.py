@@ -75,6 +75,21 @@ def _no_drop_path(m):
             mod.drop_prob = 0.0
 
 
+def _input_grad_err(a, r):
+    """(max-norm rel error, L2 rel error, fraction of voxels off by > 1e-4 of the max) of an input
+    gradient.  The conv stacks next to the input end in LeakyReLU: a pre-activation within ~1e-7 of
+    zero takes the other slope in fp32 than in fp64, and the flipped voxel's gradient differs by
+    0.8x over the few-voxel receptive field of the convs after it.  Which voxels flip depends on
+    fp32 rounding order, so the max-norm error of the input gradient alone is a lottery (1e-5 or
+    1e-3 for the same model; scripts/diag_model_kinks.py: 182 of 221184 voxels in one 7^3 box).
+    The test bounds the L2 error, the max error loosely, and requires the outliers to be local."""
+    a, r = a.detach().double(), r.detach().double().to(a.device)
+    d = (a - r).abs()
+    mx = r.abs().max().clamp_min(1e-12)
+    return (float(d.max() / mx), float(d.norm() / r.norm().clamp_min(1e-12)),
+            float((d > 1e-4 * mx).double().mean()))
+
+
 def _model_parity(device, m, ref_fn, inputs, tgt, ptol=2e-3):
     recipe.fill_params(m)
     _no_drop_path(m)
@@ -91,11 +106,12 @@ def _model_parity(device, m, ref_fn, inputs, tgt, ptol=2e-3):
     out = m(*ins)["binary_classification"]
     torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device)).backward()
     torch.cuda.synchronize()
-    gerr = [rel_err(a.grad, r.grad) for a, r in zip(ins, ins64)]
-    print(f"model parity: logits {rel_err(out, ref):.3e}, input grads {', '.join(f'{e:.3e}' for e in gerr)}")
+    gerr = [_input_grad_err(a.grad, r.grad) for a, r in zip(ins, ins64)]
+    print(f"model parity: logits {rel_err(out, ref):.3e}, input grads (max, L2, voxel fraction > 1e-4 max) "
+          f"{'; '.join(', '.join(f'{v:.3e}' for v in e) for e in gerr)}")
     assert rel_err(out, ref) < 1e-3, (out, ref)
-    for e in gerr:
-        assert e < 1e-3
+    for e_max, e_l2, frac in gerr:
+        assert e_l2 < 1e-3 and e_max < 1e-2 and frac < 0.01, (e_max, e_l2, frac)
     worst = {}
     for k, prm in m.named_parameters():
         r = p[k].grad

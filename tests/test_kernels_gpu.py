@@ -564,9 +564,11 @@ def test_linear_bwd_12x12_fused_vs_torch_fp64(device, rows, bias):
         assert rel_err(dev[2].grad, leaves[2].grad) < TOL
 
 
-@pytest.mark.parametrize("rows,residual_x", [(50003, True), (16, False), (33, True), (5, True)])
-def test_ln_mlp_vs_torch_fp64(device, rows, residual_x):
-    """norm2 + fc1 + GELU + fc2 (+ x) in one kernel per direction (mlp.hip LN prologue)."""
+@pytest.mark.parametrize("rows,residual_x,skip", [(50003, True, False), (16, False, False), (33, True, False),
+                                                   (5, True, False), (50003, True, True), (17, False, True)])
+def test_ln_mlp_vs_torch_fp64(device, rows, residual_x, skip):
+    """norm2 + fc1 + GELU + fc2 (+ x) (+ the residual group's skip) in one kernel per direction
+    (mlp.hip LN prologue; skip = mmni_ln_mlp_skip_fwd, its gradient dy)."""
     C, H = 12, 48
     gen = torch.Generator().manual_seed(rows + 17)
     x = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 1.5 - 0.3
@@ -577,12 +579,15 @@ def test_ln_mlp_vs_torch_fp64(device, rows, residual_x):
     w2 = torch.randn(C, H, generator=gen, dtype=torch.float64) * 0.2
     b2 = torch.randn(C, generator=gen, dtype=torch.float64)
     g = torch.randn(rows, C, generator=gen, dtype=torch.float64)
-    leaves = [t.clone().requires_grad_(True) for t in (x, gm, bt, w1, b1, w2, b2)]
+    sk = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 2.0
+    leaves = [t.clone().requires_grad_(True) for t in (x, gm, bt, w1, b1, w2, b2, sk)]
     F_ = torch.nn.functional
     xn = F_.layer_norm(leaves[0], (C,), leaves[1], leaves[2], 1e-5)
     ref = F_.linear(F_.gelu(F_.linear(xn, leaves[3], leaves[4])), leaves[5], leaves[6])
     if residual_x:
         ref = ref + leaves[0]
+    if skip:
+        ref = ref + leaves[7]
     (ref * g).sum().backward()
 
     class _M(torch.nn.Module):
@@ -597,13 +602,14 @@ def test_ln_mlp_vs_torch_fp64(device, rows, residual_x):
         m.fc1.weight.copy_(w1.float()); m.fc1.bias.copy_(b1.float())
         m.fc2.weight.copy_(w2.float()); m.fc2.bias.copy_(b2.float())
     xd = x.float().to(device).requires_grad_(True)
+    sd = sk.float().to(device).requires_grad_(True) if skip else None
     assert MF.ln_mlp_ok(xd, norm, m)
-    out = MF.ln_mlp(xd, norm, m, residual_x=residual_x)
+    out = MF.ln_mlp(xd, norm, m, residual_x=residual_x, skip=sd)
     (out * g.float().to(device)).sum().backward()
     torch.cuda.synchronize()
     assert rel_err(out, ref) < TOL
     got = [xd.grad, norm.weight.grad, norm.bias.grad, m.fc1.weight.grad, m.fc1.bias.grad, m.fc2.weight.grad,
-           m.fc2.bias.grad]
+           m.fc2.bias.grad] + ([sd.grad] if skip else [])
     for a, r in zip(got, leaves):
         assert rel_err(a, r.grad) < TOL
 
