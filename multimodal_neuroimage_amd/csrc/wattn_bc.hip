@@ -485,6 +485,14 @@ __device__ __forceinline__ float reduce32(f2 (&P)[16], int lane) {
 }
 }  // namespace q4
 
+// a zero f2 in one 64-bit move: the spare lanes' partials (the compiler splits a plain f2 zero
+// into two 32-bit moves, 32 per step)
+__device__ __forceinline__ f2 zero2() {
+    double r;
+    asm volatile("v_mov_b64 %0, 0" : "=v"(r));
+    return __builtin_bit_cast(f2, r);
+}
+
 template <bool MASKED, bool FOLD>
 __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
                                          const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
@@ -520,7 +528,7 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
                 // all lanes, with zero rows, the compiler spilled ~800 VGPRs; the branch does not)
                 f2 P[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) P[i] = bc::splat(0.f);
+                for (int i = 0; i < 16; ++i) P[i] = zero2();
                 if (lane_ok) {
                     char* dp = sm + dto + trow;
                     // this step's table-gradient entries (after the previous step's stores: see dto)
