@@ -292,6 +292,14 @@ int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, 
                        const float* rstd, const float* gamma, const float* beta, const float* w,
                        const float* dres, float* dx, float* dw, float* db, float* dgamma,
                        float* dbeta, void* workspace, void* stream);
+/* ln_linear_bwd with a second residual gradient: dx = LN_bwd(dy W) + dres + dres2 (each nullable).
+ * dres2 carries the gradient of the identity skip of the residual group this block opens (RSTB /
+ * CRSTB `residual_group(x) + x`, swinfusion_module.py:814,918-927), which would otherwise meet dx
+ * in a separate full-size add. */
+int mmni_ln_linear_bwd2(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                        const float* rstd, const float* gamma, const float* beta, const float* w,
+                        const float* dres, const float* dres2, float* dx, float* dw, float* db, float* dgamma,
+                        float* dbeta, void* workspace, void* stream);
 int mmni_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* w,
                     float* dx, float* dw, float* db, void* workspace, void* stream);
 

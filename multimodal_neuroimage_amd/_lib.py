@@ -103,6 +103,7 @@ SIGNATURES = {
     "mmni_ln_linear_fwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 9),
     "mmni_tok_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(TokDesc)]),
     "mmni_ln_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 15),
+    "mmni_ln_linear_bwd2": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 16),
     "mmni_linear_bwd": (_c_int, [ctypes.POINTER(TokDesc)] + [_vp] * 8),
 }
 

@@ -49,6 +49,7 @@ struct TokArgs {
     float* rstd;         // (rows)
     const float* dy;     // bwd: (rows, N)
     const float* dres;   // bwd: (rows, C) residual gradient added to dx, or null
+    const float* dres2;  // bwd: a second one (the residual group's skip), or null
     float* dx;           // bwd: (rows, C)
     float* partA;        // [waves][N*C + N (+ 2C)]  dW | db (| dgamma | dbeta)
     float* partB;        // unused (dgamma | dbeta follow dW | db in partA's rows)
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
             const f4 xh = ok ? (xc[u] - mu[u]) * ru[u] : zero4();
             f4 dx = ln_bwd_chunk(dxn, xh, gm4, ru[u]);
             if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
+            if (a.dres2 != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres2 + (t0 + t) * C + 4 * g);
             if (ok) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
             dg += dxn * xh;
             dbt += dxn;
@@ -363,19 +365,20 @@ extern "C" size_t mmni_tok_bwd_workspace_bytes(const mmni_tok_desc* d) {
     return waves * ((size_t)d->N * d->C + d->N + 2 * d->C) * sizeof(float);
 }
 
-extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
-                                  const float* rstd, const float* gamma, const float* beta, const float* w,
-                                  const float* dres, float* dx, float* dw, float* db, float* dgamma, float* dbeta,
-                                  void* workspace, void* stream) {
+static int ln_linear_bwd_impl(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                              const float* rstd, const float* gamma, const float* beta, const float* w,
+                              const float* dres, const float* dres2, float* dx, float* dw, float* db, float* dgamma,
+                              float* dbeta, void* workspace, void* stream) {
     int rc = tok_check(d, true);
     if (rc) return rc;
     MMNI_ARG_CHECK(dy && x && mean && rstd && gamma && beta && w && dx && dw && dgamma && dbeta && workspace,
                    "ln_linear_bwd: null pointer");
-    MMNI_ARG_CHECK(al16(x) && al16(dx) && (!dres || al16(dres)), "ln_linear_bwd: rows must be 16-byte aligned");
+    MMNI_ARG_CHECK(al16(x) && al16(dx) && (!dres || al16(dres)) && (!dres2 || al16(dres2)),
+                   "ln_linear_bwd: rows must be 16-byte aligned");
     const int N = d->N, C = d->C;
     blk::TokArgs a{};
     a.rows = d->rows; a.x = x; a.gamma = gamma; a.beta = beta; a.w = w; a.mean = const_cast<float*>(mean);
-    a.rstd = const_cast<float*>(rstd); a.dy = dy; a.dres = dres; a.dx = dx;
+    a.rstd = const_cast<float*>(rstd); a.dy = dy; a.dres = dres; a.dres2 = dres2; a.dx = dx;
     hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (d->rows + 15) / 16;
     int waves = 0;
@@ -403,6 +406,22 @@ extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const
     segs.dst[3] = dbeta;
     column_sum_segs(a.partA, waves, N * C + N + 2 * C, segs, s);
     return launch_status("ln_linear_bwd_colsum");
+}
+
+extern "C" int mmni_ln_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                                  const float* rstd, const float* gamma, const float* beta, const float* w,
+                                  const float* dres, float* dx, float* dw, float* db, float* dgamma, float* dbeta,
+                                  void* workspace, void* stream) {
+    return ln_linear_bwd_impl(d, dy, x, mean, rstd, gamma, beta, w, dres, nullptr, dx, dw, db, dgamma, dbeta,
+                              workspace, stream);
+}
+
+extern "C" int mmni_ln_linear_bwd2(const mmni_tok_desc* d, const float* dy, const float* x, const float* mean,
+                                   const float* rstd, const float* gamma, const float* beta, const float* w,
+                                   const float* dres, const float* dres2, float* dx, float* dw, float* db,
+                                   float* dgamma, float* dbeta, void* workspace, void* stream) {
+    return ln_linear_bwd_impl(d, dy, x, mean, rstd, gamma, beta, w, dres, dres2, dx, dw, db, dgamma, dbeta,
+                              workspace, stream);
 }
 
 extern "C" int mmni_linear_bwd(const mmni_tok_desc* d, const float* dy, const float* x, const float* w, float* dx,

@@ -787,9 +787,11 @@ def _tok_desc(rows, C, N, eps=0.0):
 
 class _LnLinear(torch.autograd.Function):
     """y = LN(x) W^T + b in one pass; the LayerNorm output never reaches HBM (the backward
-    recomputes it from x and the saved row statistics).  With passthrough=True the Function also
+    recomputes it from x and the saved row statistics).  With passthrough=1 the Function also
     returns x itself (a view) to be used as the block's residual: its gradient arrives here and is
-    added inside the fused backward instead of by a separate autograd add."""
+    added inside the fused backward instead of by a separate autograd add.  passthrough=2 returns
+    a second view for the identity skip of the residual group this block opens (RSTB / CRSTB),
+    whose gradient joins in the same kernel (mmni_ln_linear_bwd2)."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, w, b, eps, passthrough):
@@ -810,15 +812,18 @@ class _LnLinear(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.xshape = x.shape
         y = y.view(*x.shape[:-1], N)
+        if passthrough == 2:
+            return y, x.view(x.shape), x.view(x.shape)
         return (y, x.view(x.shape)) if passthrough else y
 
     @staticmethod
-    def backward(ctx, dy, dres=None):
+    def backward(ctx, dy, dres=None, dres2=None):
         x2, gamma, beta, w, mean, rstd = ctx.saved_tensors
         N, C = w.shape
         rows = x2.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
         dr2 = dres.reshape(-1, C).contiguous() if dres is not None else None
+        ds2 = dres2.reshape(-1, C).contiguous() if dres2 is not None else None
         dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
         dw = torch.empty_like(w)
         db = torch.empty(N, device=x2.device, dtype=torch.float32) if ctx.has_b else None
@@ -828,11 +833,17 @@ class _LnLinear(torch.autograd.Function):
         d = _tok_desc(rows, C, N)
         ws = torch.empty(L.mmni_tok_bwd_workspace_bytes(ctypes.byref(d)) // 4, device=x2.device, dtype=torch.float32)
         ev = KernelTimer.start()
-        check(L.mmni_ln_linear_bwd(ctypes.byref(d), ptr(dy2), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
-                                   ptr(w), ptr(dr2), ptr(dx), ptr(dw), ptr(db), ptr(dgamma), ptr(dbeta), ptr(ws),
-                                   stream_handle(x2.device)), "mmni_ln_linear_bwd")
+        if ds2 is None:
+            check(L.mmni_ln_linear_bwd(ctypes.byref(d), ptr(dy2), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma),
+                                       ptr(beta), ptr(w), ptr(dr2), ptr(dx), ptr(dw), ptr(db), ptr(dgamma), ptr(dbeta),
+                                       ptr(ws), stream_handle(x2.device)), "mmni_ln_linear_bwd")
+        else:
+            check(L.mmni_ln_linear_bwd2(ctypes.byref(d), ptr(dy2), ptr(x2), ptr(mean), ptr(rstd), ptr(gamma),
+                                        ptr(beta), ptr(w), ptr(dr2), ptr(ds2), ptr(dx), ptr(dw), ptr(db), ptr(dgamma),
+                                        ptr(dbeta), ptr(ws), stream_handle(x2.device)), "mmni_ln_linear_bwd2")
+        nres = (dr2 is not None) + (ds2 is not None)
         KernelTimer.stop(f"ln_linear_bwd_{C}x{N}", ev, 4.0 * rows * C * N + 16.0 * rows * C,
-                         4.0 * rows * (N + 2 * C + 2 + (C if dr2 is not None else 0)))
+                         4.0 * rows * (N + 2 * C + 2 + C * nres))
         return dx.view(ctx.xshape), dgamma, dbeta, dw, db, None, None
 
 
@@ -843,12 +854,14 @@ def ln_linear_ok(x, norm, lin):
 
 def ln_linear(x, norm, lin, passthrough=False):
     """lin(norm(x)) fused (x (..., 12), lin 12 -> 12/24/36); other shapes run LayerNorm and Linear
-    as separate HIP kernels.  passthrough=True also returns x for use as the residual (see
-    _LnLinear)."""
+    as separate HIP kernels.  passthrough=True (1) also returns x for use as the residual, 2 returns
+    it twice (residual, residual-group skip) (see _LnLinear)."""
     require_device(x, what="ln_linear")
     if ln_linear_ok(x, norm, lin):
-        return _LnLinear.apply(x, norm.weight, norm.bias, lin.weight, lin.bias, float(norm.eps), passthrough)
+        return _LnLinear.apply(x, norm.weight, norm.bias, lin.weight, lin.bias, float(norm.eps), int(passthrough))
     y = linear(layer_norm(x, norm), lin)
+    if passthrough == 2:
+        return y, x, x
     return (y, x) if passthrough else y
 
 

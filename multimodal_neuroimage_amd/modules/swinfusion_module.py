@@ -197,16 +197,29 @@ class SwinTransformerBlock_fusion(nn.Module):
         nd = len(x_size)
         return shift_mask_buffer(tuple(x_size), to_ntuple(self.window_size, nd), to_ntuple(self.shift_size, nd))
 
-    def forward(self, x, x_size, skip=None):
+    def forward(self, x, x_size, skip=None, emit_skip=0):
         """skip: the identity skip of the residual group this block ends (RSTB / CRSTB), added in
-        the MLP epilogue when the fused path runs (one full-size add less per group)."""
+        the MLP epilogue when the fused path runs (one full-size add less per group).
+        emit_skip (the group's first block): 1 also returns the group input as a second view out
+        of norm1 + qkv, to be the last block's skip, so that the skip's gradient joins this block's
+        input gradient inside the LN + Linear backward (no autograd add); 2 does the same for a
+        one-block group and uses the view as this block's own skip."""
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
+        xs = x
         if inactive(self.drop_path) and ln_linear_ok(x, self.norm1, self.attn.qkv):
             # norm1 + qkv in one kernel; the residual's gradient joins inside its backward
-            qkv, xr = ln_linear(x, self.norm1, self.attn.qkv, passthrough=True)
+            if emit_skip:
+                qkv, xr, xs = ln_linear(x, self.norm1, self.attn.qkv, passthrough=2)
+            else:
+                qkv, xr = ln_linear(x, self.norm1, self.attn.qkv, passthrough=True)
+            if emit_skip == 2:
+                skip = xs
             x = self.attn.attend(qkv.reshape(B * L, 3 * C), geom, residual=xr.reshape(B * L, C)).view(B, L, C)
-            return ln_mlp(x, self.norm2, self.mlp, skip=skip)   # x + mlp(norm2(x)) [+ skip], one kernel
+            out = ln_mlp(x, self.norm2, self.mlp, skip=skip)   # x + mlp(norm2(x)) [+ skip], one kernel
+            return (out, xs) if emit_skip == 1 else out
+        if emit_skip == 2:
+            skip = x
         xn = layer_norm(x, self.norm1).reshape(B * L, C)
         if inactive(self.drop_path):   # residual adds fused into the proj / fc2 epilogues
             x = self.attn.forward_tokens(xn, geom, residual=x.reshape(B * L, C)).view(B, L, C)
@@ -214,7 +227,8 @@ class SwinTransformerBlock_fusion(nn.Module):
         else:
             x = x + self.drop_path(self.attn.forward_tokens(xn, geom).view(B, L, C))
             x = x + self.drop_path(self.mlp(layer_norm(x, self.norm2)))
-        return x if skip is None else x + skip
+        out = x if skip is None else x + skip
+        return (out, xs) if emit_skip == 1 else out
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads={self.num_heads}, "
@@ -256,24 +270,35 @@ class Cross_SwinTransformerBlock(nn.Module):
         nd = len(x_size)
         return shift_mask_buffer(tuple(x_size), to_ntuple(self.window_size, nd), to_ntuple(self.shift_size, nd))
 
-    def forward(self, x, y, x_size, skip=None):
+    def forward(self, x, y, x_size, skip=None, emit_skip=0):
         """skip: (skip_x, skip_y), the identity skips of the CRSTB inter-modal group this block
-        ends, added in the MLP epilogues on the fused path."""
+        ends, added in the MLP epilogues on the fused path.  emit_skip as in
+        SwinTransformerBlock_fusion, for the pair (x, y)."""
         sx, sy = skip if skip is not None else (None, None)
+        xs, ys = x, y
         B, L, C = x.shape
         geom = geometry(B, x_size, self.window_size, self.shift_size)
         if (inactive(self.drop_path_A) and inactive(self.drop_path_B)
                 and ln_linear_ok(x, self.norm1_A, self.attn_A.q) and ln_linear_ok(x, self.norm1_A, self.attn_B.kv)):
             # norm1 fused into each projection that reads it (x -> q_A, kv_B; y -> q_B, kv_A)
-            qa, xr = ln_linear(x, self.norm1_A, self.attn_A.q, passthrough=True)
+            if emit_skip:
+                qa, xr, xs = ln_linear(x, self.norm1_A, self.attn_A.q, passthrough=2)
+                qb, yr, ys = ln_linear(y, self.norm1_B, self.attn_B.q, passthrough=2)
+            else:
+                qa, xr = ln_linear(x, self.norm1_A, self.attn_A.q, passthrough=True)
+                qb, yr = ln_linear(y, self.norm1_B, self.attn_B.q, passthrough=True)
+            if emit_skip == 2:
+                sx, sy = xs, ys
             kvb = ln_linear(x, self.norm1_A, self.attn_B.kv)
-            qb, yr = ln_linear(y, self.norm1_B, self.attn_B.q, passthrough=True)
             kva = ln_linear(y, self.norm1_B, self.attn_A.kv)
             xa = self.attn_A.attend(qa.reshape(B * L, C), kva.reshape(B * L, 2 * C), geom,
                                     residual=xr.reshape(B * L, C)).view(B, L, C)
             yb = self.attn_B.attend(qb.reshape(B * L, C), kvb.reshape(B * L, 2 * C), geom,
                                     residual=yr.reshape(B * L, C)).view(B, L, C)
-            return ln_mlp(xa, self.norm2_A, self.mlp_A, skip=sx), ln_mlp(yb, self.norm2_B, self.mlp_B, skip=sy)
+            out = ln_mlp(xa, self.norm2_A, self.mlp_A, skip=sx), ln_mlp(yb, self.norm2_B, self.mlp_B, skip=sy)
+            return (out, (xs, ys)) if emit_skip == 1 else out
+        if emit_skip == 2:
+            sx, sy = x, y
         xn = layer_norm(x, self.norm1_A).reshape(B * L, C)
         yn = layer_norm(y, self.norm1_B).reshape(B * L, C)
         if inactive(self.drop_path_A) and inactive(self.drop_path_B):   # fused residual adds
@@ -288,7 +313,8 @@ class Cross_SwinTransformerBlock(nn.Module):
             x = x + self.drop_path_A(self.mlp_A(layer_norm(x, self.norm2_A)))
             y = y + self.drop_path_B(b)
             y = y + self.drop_path_B(self.mlp_B(layer_norm(y, self.norm2_B)))
-        return (x if sx is None else x + sx), (y if sy is None else y + sy)
+        out = (x if sx is None else x + sx), (y if sy is None else y + sy)
+        return (out, (xs, ys)) if emit_skip == 1 else out
 
     def extra_repr(self):
         return (f"dim={self.dim}, input_resolution={self.input_resolution}, num_heads={self.num_heads}, "
@@ -338,11 +364,23 @@ class BasicLayer_fusion(nn.Module):
 
     def forward(self, x, x_size, skip=None):
         """skip: the enclosing residual group's identity skip (RSTB / CRSTB), handed to the last
-        block so it joins that block's MLP epilogue; added after the downsample when there is one."""
+        block so it joins that block's MLP epilogue; added after the downsample when there is one.
+        When the skip is the group's own input, the first block re-emits it as a view of its
+        norm1 + qkv (emit_skip) so the skip's gradient joins inside that block's backward."""
         last = len(self.blocks) - 1
+        fold = skip is not None and skip is x and self.downsample is None and last >= 0
+
+        def run(blk, *args):
+            return checkpoint.checkpoint(blk, *args, use_reentrant=False) if self.use_checkpoint else blk(*args)
         for i, blk in enumerate(self.blocks):
+            if fold and i == 0:
+                if last == 0:
+                    x = run(blk, x, x_size, None, 2)
+                else:
+                    x, skip = run(blk, x, x_size, None, 1)
+                continue
             s = skip if (i == last and self.downsample is None) else None
-            x = checkpoint.checkpoint(blk, x, x_size, s, use_reentrant=False) if self.use_checkpoint else blk(x, x_size, s)
+            x = run(blk, x, x_size, s)
         if self.downsample is not None:
             x = self.downsample(x)
             return x if skip is None else x + skip
@@ -374,14 +412,22 @@ class Cross_BasicLayer(nn.Module):
         self.downsample = downsample(input_resolution, dim=dim, norm_layer=norm_layer) if downsample else None
 
     def forward(self, x, y, x_size, skip=None):
-        """skip: (skip_x, skip_y) of the enclosing CRSTB, joined in the last block's MLP epilogues."""
+        """skip: (skip_x, skip_y) of the enclosing CRSTB, joined in the last block's MLP epilogues
+        (re-emitted by the first block when it is the group's input, as in BasicLayer_fusion)."""
         last = len(self.blocks) - 1
+        fold = (skip is not None and skip[0] is x and skip[1] is y and self.downsample is None and last >= 0)
+
+        def run(blk, *args):
+            return checkpoint.checkpoint(blk, *args, use_reentrant=False) if self.use_checkpoint else blk(*args)
         for i, blk in enumerate(self.blocks):
+            if fold and i == 0:
+                if last == 0:
+                    x, y = run(blk, x, y, x_size, None, 2)
+                else:
+                    (x, y), skip = run(blk, x, y, x_size, None, 1)
+                continue
             s = skip if (i == last and self.downsample is None) else None
-            if self.use_checkpoint:
-                x, y = checkpoint.checkpoint(blk, x, y, x_size, s, use_reentrant=False)
-            else:
-                x, y = blk(x, y, x_size, s)
+            x, y = run(blk, x, y, x_size, s)
         if self.downsample is not None:
             x, y = self.downsample(x), self.downsample(y)
             if skip is not None:

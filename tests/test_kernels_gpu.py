@@ -486,10 +486,12 @@ def test_fused_mlp_weight_grad_is_deterministic(device):
 
 
 @pytest.mark.parametrize("N", [12, 24, 36])
-@pytest.mark.parametrize("rows,passthrough", [(50003, True), (16, False), (33, True), (7, False)])
+@pytest.mark.parametrize("rows,passthrough", [(50003, True), (16, False), (33, True), (7, False), (50003, 2),
+                                              (17, 2)])
 def test_ln_linear_vs_torch_fp64(device, N, rows, passthrough):
     """norm1 + qkv/q/kv fused (blockops.hip): LN output never stored, backward recomputes it and
-    adds the residual gradient (passthrough) in the same pass."""
+    adds the residual gradient (passthrough) in the same pass; passthrough=2 adds a second one (the
+    residual group's skip, mmni_ln_linear_bwd2)."""
     C = 12
     gen = torch.Generator().manual_seed(rows * 3 + N)
     x = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 2 + 0.5
@@ -499,10 +501,12 @@ def test_ln_linear_vs_torch_fp64(device, N, rows, passthrough):
     b = torch.randn(N, generator=gen, dtype=torch.float64)
     g = torch.randn(rows, N, generator=gen, dtype=torch.float64)
     gr = torch.randn(rows, C, generator=gen, dtype=torch.float64)
+    gs = torch.randn(rows, C, generator=gen, dtype=torch.float64) * 3.0
     leaves = [t.clone().requires_grad_(True) for t in (x, gm, bt, w, b)]
     F_ = torch.nn.functional
     ref = F_.linear(F_.layer_norm(leaves[0], (C,), leaves[1], leaves[2], 1e-5), leaves[3], leaves[4])
-    ((ref * g).sum() + ((leaves[0] * gr).sum() if passthrough else 0)).backward()
+    ((ref * g).sum() + ((leaves[0] * gr).sum() if passthrough else 0)
+     + ((leaves[0] * gs).sum() if passthrough == 2 else 0)).backward()
     norm, lin = torch.nn.LayerNorm(C).to(device), torch.nn.Linear(C, N).to(device)
     with torch.no_grad():
         norm.weight.copy_(gm.float()); norm.bias.copy_(bt.float())
@@ -510,7 +514,12 @@ def test_ln_linear_vs_torch_fp64(device, N, rows, passthrough):
     xd = x.float().to(device).requires_grad_(True)
     assert MF.ln_linear_ok(xd, norm, lin)
     out = MF.ln_linear(xd, norm, lin, passthrough=passthrough)
-    if passthrough:
+    if passthrough == 2:
+        out, xr, xs = out
+        assert xr.data_ptr() == xd.data_ptr() and xs.data_ptr() == xd.data_ptr()
+        loss = ((out * g.float().to(device)).sum() + (xr * gr.float().to(device)).sum()
+                + (xs * gs.float().to(device)).sum())
+    elif passthrough:
         out, xr = out
         assert xr.data_ptr() == xd.data_ptr()
         loss = (out * g.float().to(device)).sum() + (xr * gr.float().to(device)).sum()
