@@ -14,6 +14,7 @@
 // The weight is addressed as W(n, k) = w[n*w_sn + k*w_sk]: (K, 1) is an nn.Linear weight, (1, Nw)
 // its transpose, used for dX = dY W.
 #include "mmni_common.h"
+#include "tokentile.h"
 
 namespace mmni {
 
@@ -231,12 +232,16 @@ extern "C" int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const 
                    "token_linear: residual needs epi 0/1 and 16-byte alignment");
     a.x = x; a.w = w; a.bias = bias; a.aux = aux; a.w2 = w2; a.b2 = b2; a.res = residual; a.y = y;
     const int64_t blocks = (d->rows + 255) / 256;
-    const int grid = (int)(blocks < 4096 ? blocks : 4096);
     hipStream_t s = (hipStream_t)stream;
-#define MMNI_TLIN(K_, N_, E_, K2_)                                                    \
-    if (d->K == K_ && d->N == N_ && d->epi == E_ && (E_ != 2 || d->K2 == K2_)) {      \
-        token_linear_kernel<K_, N_, E_, K2_><<<grid, 256, 0, s>>>(a);                  \
-        return launch_status("token_linear");                                         \
+    // grid-stride loops over row tiles: one resident wave of blocks (a fixed 4096-block grid left
+    // a partial second round of blocks on every CU)
+#define MMNI_TLIN(K_, N_, E_, K2_)                                                                  \
+    if (d->K == K_ && d->N == N_ && d->epi == E_ && (E_ != 2 || d->K2 == K2_)) {                    \
+        static const int resident =                                                                \
+            tt::resident_blocks(reinterpret_cast<const void*>(&token_linear_kernel<K_, N_, E_, K2_>), 256, 0); \
+        const int grid = (int)(blocks < resident ? blocks : resident);                              \
+        token_linear_kernel<K_, N_, E_, K2_><<<grid, 256, 0, s>>>(a);                                \
+        return launch_status("token_linear");                                                       \
     }
     MMNI_TLIN(12, 36, 0, 0) MMNI_TLIN(12, 12, 0, 0) MMNI_TLIN(12, 24, 0, 0) MMNI_TLIN(12, 48, 0, 0)
     MMNI_TLIN(48, 12, 0, 0) MMNI_TLIN(36, 12, 0, 0) MMNI_TLIN(24, 12, 0, 0)
