@@ -135,10 +135,18 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
 // ------------------------------------------------------------------------------------
 // dx = LN_bwd(dy W) + dres;  dW = dy^T LN(x),  db = colsum dy,  dgamma, dbeta
 // ------------------------------------------------------------------------------------
+#ifndef MMNI_LLB_EARLY_RES
+#define MMNI_LLB_EARLY_RES 1
+#endif
+#ifndef MMNI_LLB36_WAVES
+#define MMNI_LLB36_WAVES 3
+#endif
 template <int N, int U>
-__global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N == 36 ? MMNI_LLB36_WAVES : 1)))
+void ln_linear_bwd_kernel(TokArgs a) {
     constexpr int NT = (N + 15) / 16;
     constexpr int NS = N / 4;   // k-steps over the N gradient columns
+    constexpr bool kEarlyRes = MMNI_LLB_EARLY_RES && N == 36;   // (N = 12 would drop to 3 waves / SIMD)
     const int lane = threadIdx.x & 63;
     const Tile tl{a.rows, lane & 15, lane >> 4};
     const int t = tl.t, g = tl.g;
@@ -167,7 +175,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
     // U consecutive tiles per step, all loads first (see ln_linear_fwd_kernel)
     for (int64_t tb = wave * U; tb < tiles; tb += nwaves * U) {
         float dyb[U][NS], xa[U][4], mt[U][4], rt[U][4], dya[U][NT][4], mu[U], ru[U];
-        f4 xc[U];
+        f4 xc[U], rs[U], rs2[U];
         if constexpr (kDyLds) {
             // dy tiles (16 x N floats, contiguous) in with 16-B loads, both operand maps out of LDS
             f4 dv[U][DYV];
@@ -208,6 +216,10 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
             mu[u] = tok ? a.mean[t0 + t] : 0.f;
             ru[u] = tok ? a.rstd[t0 + t] : 0.f;
             xc[u] = ok ? *reinterpret_cast<const f4*>(a.x + (t0 + t) * C + 4 * g) : zero4();
+            if (kEarlyRes) {   // the residual gradients travel with the tile's other loads
+                rs[u] = (a.dres != nullptr && ok) ? *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g) : zero4();
+                rs2[u] = (a.dres2 != nullptr && ok) ? *reinterpret_cast<const f4*>(a.dres2 + (t0 + t) * C + 4 * g) : zero4();
+            }
             tl.load_tm<C>(a.x, t0, 0, C, xa[u]);
             tl.load_tm_scalar(a.mean, t0, mt[u]);
             tl.load_tm_scalar(a.rstd, t0, rt[u]);
@@ -227,8 +239,12 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(TokArgs a) {
             const bool ok = tl.chunk_ok(t0);
             const f4 xh = ok ? (xc[u] - mu[u]) * ru[u] : zero4();
             f4 dx = ln_bwd_chunk(dxn, xh, gm4, ru[u]);
-            if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
-            if (a.dres2 != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres2 + (t0 + t) * C + 4 * g);
+            if (kEarlyRes) {
+                dx += rs[u] + rs2[u];
+            } else {
+                if (a.dres != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres + (t0 + t) * C + 4 * g);
+                if (a.dres2 != nullptr && ok) dx += *reinterpret_cast<const f4*>(a.dres2 + (t0 + t) * C + 4 * g);
+            }
             if (ok) *reinterpret_cast<f4*>(a.dx + (t0 + t) * C + 4 * g) = dx;
             dg += dxn * xh;
             dbt += dxn;
