@@ -326,6 +326,19 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
         io.load_fm(a.dy, t0, dyb);
         io.load_tm(a.x, t0, xa);
         io.load_tm(a.dy, t0, dya);
+#ifndef MMNI_MLP_BWD_EARLY
+#define MMNI_MLP_BWD_EARLY 1
+#endif
+        // LN variant: the chunk-layout x and dy rows of the LN backward / residual gradient load
+        // with the tile's operands (after the MFMAs their latency was exposed once per tile)
+        f4 xc_e = (f4){0.f, 0.f, 0.f, 0.f}, dyr_e = xc_e;
+        if constexpr (LN && MMNI_MLP_BWD_EARLY) {
+            if (io.row_ok(t0)) {
+                const int64_t roff = (t0 + li) * C + 4 * lg;
+                xc_e = *reinterpret_cast<const f4*>(a.x + roff);
+                if (a.res_x) dyr_e = *reinterpret_cast<const f4*>(a.dy + roff);
+            }
+        }
         float mean = 0.f, rstd = 0.f;
         if constexpr (LN) {
             // recompute the LN of the tile: feature-major operand, and the token-major copy for
@@ -375,13 +388,14 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
             const bool ok = io.row_ok(t0);
             const int64_t roff = (t0 + li) * C + 4 * lg;
             const f4 dxn = dxo[0] + dxo[1] + dxo[2];
-            const f4 xc = ok ? *reinterpret_cast<const f4*>(a.x + roff) : (f4){0.f, 0.f, 0.f, 0.f};
+            const f4 xc = MMNI_MLP_BWD_EARLY ? xc_e : ok ? *reinterpret_cast<const f4*>(a.x + roff) : (f4){0.f, 0.f, 0.f, 0.f};
             const f4 xh = ok ? (xc - mean) * rstd : (f4){0.f, 0.f, 0.f, 0.f};
             const f4 gd = dxn * gm4;
             const float s1 = sum_groups(gd[0] + gd[1] + gd[2] + gd[3]) * (1.0f / C);
             const float s2 = sum_groups(gd[0] * xh[0] + gd[1] * xh[1] + gd[2] * xh[2] + gd[3] * xh[3]) * (1.0f / C);
             f4 dxv = (gd - s1 - xh * s2) * rstd;
-            if (a.res_x && ok) dxv += *reinterpret_cast<const f4*>(a.dy + roff);
+            if (MMNI_MLP_BWD_EARLY) dxv += dyr_e;
+            else if (a.res_x && ok) dxv += *reinterpret_cast<const f4*>(a.dy + roff);
             if (ok) *reinterpret_cast<f4*>(a.dx + roff) = dxv;
             dgm += dxn * xh;
             dbt += dxn;
