@@ -204,6 +204,41 @@ __global__ __launch_bounds__(256) void token_linear_kernel(TLinArgs a) {
     }
 }
 
+// 12 -> 12 Linear (+ bias, + residual) on contiguous rows (the attention proj): one 16-token tile
+// per wave step on the f32 MFMA in the accumulator-chunk layout of tokentile.h (as blockops'
+// linear_bwd), y^T = W x^T.  No LDS staging and no block barriers: the LDS-tiled path above
+// moved the same bytes at ~3.7 TB/s.
+#ifndef MMNI_TLIN12_MFMA
+#define MMNI_TLIN12_MFMA 1
+#endif
+__global__ __launch_bounds__(256) void linear12_fwd_kernel(TLinArgs a) {
+    using namespace tt;
+    const int lane = threadIdx.x & 63;
+    const Tile tl{a.rows, lane & 15, lane >> 4};
+    const int t = tl.t, g = tl.g;
+    const int64_t wave = __builtin_amdgcn_readfirstlane(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    float wf[CS];   // A operand: W[o = t][c = 4 s + g]
+#pragma unroll
+    for (int s = 0; s < CS; ++s) wf[s] = t < C ? a.w[t * a.w_sn + (4 * s + g) * a.w_sk] : 0.f;
+    f4 bc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bc[i] = (g < 3 && a.bias != nullptr) ? a.bias[4 * g + i] : 0.f;
+    const int64_t tiles = (a.rows + 15) / 16;
+    for (int64_t tile = wave; tile < tiles; tile += nwaves) {
+        const int64_t t0 = tile * 16;
+        float xb[CS];
+        tl.load_fm<CS, C>(a.x, t0, xb);
+        const bool ok = tl.chunk_ok(t0);
+        const int64_t off = (t0 + t) * C + 4 * g;
+        const f4 r = (a.res != nullptr && ok) ? *reinterpret_cast<const f4*>(a.res + off) : zero4();
+        f4 y = bc;
+#pragma unroll
+        for (int s = 0; s < CS; ++s) y = mfma(wf[s], xb[s], y);
+        if (ok) *reinterpret_cast<f4*>(a.y + off) = y + r;
+    }
+}
+
 }  // namespace mmni
 
 using namespace mmni;
@@ -233,6 +268,14 @@ extern "C" int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const 
     a.x = x; a.w = w; a.bias = bias; a.aux = aux; a.w2 = w2; a.b2 = b2; a.res = residual; a.y = y;
     const int64_t blocks = (d->rows + 255) / 256;
     hipStream_t s = (hipStream_t)stream;
+    if (MMNI_TLIN12_MFMA && d->K == 12 && d->N == 12 && d->epi == 0 && d->ldx == 12 && d->ldy == 12) {
+        static const int resident =
+            tt::resident_blocks(reinterpret_cast<const void*>(&linear12_fwd_kernel), 256, 0);
+        const int64_t need = (d->rows + 63) / 64;   // 4 waves x 16-token tiles per block
+        const int grid = (int)(need < resident ? need : resident);
+        linear12_fwd_kernel<<<grid, 256, 0, s>>>(a);
+        return launch_status("token_linear");
+    }
     // grid-stride loops over row tiles: one resident wave of blocks (a fixed 4096-block grid left
     // a partial second round of blocks on every CU)
 #define MMNI_TLIN(K_, N_, E_, K2_)                                                                  \
