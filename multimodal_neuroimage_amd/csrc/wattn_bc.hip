@@ -580,7 +580,9 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
                 const int r0 = __builtin_amdgcn_readlane(rowk[0], owner), r1 = __builtin_amdgcn_readlane(rowk[1], owner);
                 const int r2 = __builtin_amdgcn_readlane(rowk[2], owner), r3 = __builtin_amdgcn_readlane(rowk[3], owner);
                 const int r = vsel == 0 ? r0 : (vsel == 1 ? r1 : (vsel == 2 ? r2 : r3));
-                if ((lane & 1) == 0) kout[(int64_t)r * kstride] = sum * kscale;
+                // 24-bit multiply (full rate; the 64-bit product took two v_mul_lo_u32 and a
+                // v_mad_u64_u32): the host routes row counts / strides past 2^23 / 2^31 elsewhere
+                if ((lane & 1) == 0) kout[(uint32_t)__mul24(r, (int)kstride)] = sum * kscale;
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
