@@ -707,8 +707,11 @@ constexpr int REC = 108 * 64;          // records of one window (pair t: keys t,
 constexpr int SLOT = REC + 16;         // ring stride: consecutive slots 16 B apart modulo 128 B
 }  // namespace fs
 
+#ifndef MMNI_FS_WAVES
+#define MMNI_FS_WAVES 4
+#endif
 template <int WD, int WH, int WW>
-__global__ __launch_bounds__(fs::WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(fs::WAVES * 64) __attribute__((amdgpu_waves_per_eu(MMNI_FS_WAVES)))
 void wattn_fwd_bcs_kernel(WAArgs a) {
     using Wn = bc::Win<WD, WH, WW>;
     constexpr int H = Wn::H, TSZ = Wn::TSZ;
@@ -897,7 +900,7 @@ int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     if (MMNI_FWD_STREAM) {
         const size_t lds = (size_t)bc::align4(kTsz666 * 2) * 4 + (size_t)fs::RING * fs::SLOT +
                            (size_t)(2 * fs::WAVES + 4 * fs::RING) * 4;
-        int per = (4 * kNumCU) / (8 * NHG);   // four 4-wave workgroups per CU (LDS, 128 VGPRs)
+        int per = (MMNI_FS_WAVES * kNumCU) / (8 * NHG);   // 4-wave workgroups per CU (one per wave/SIMD)
         if (per < 1) per = 1;
         wattn_fwd_bcs_kernel<6, 6, 6><<<8 * NHG * per, fs::WAVES * 64, lds, s>>>(a);
         return launch_status("wattn_fwd_bcs");
