@@ -149,3 +149,39 @@ def test_swin_v2_c2_96_b4_vs_fp64_oracle(device):
     worst = _model_parity(device, m, lambda p, a: OM.swin_v2_logits(p, "", a, 8, 6), [x],
                           torch.tensor([[1.0], [0.0], [1.0], [1.0]]))
     assert any("layers.2.blocks.5" in k for k in worst)
+
+
+def test_swinfusion3d_checkpointed_blocks_match_plain(device):
+    """use_checkpoint=True (torch.utils.checkpoint per block, swinfusion_module.py:657-665) gives the
+    same logits and gradients as the plain forward, including the residual-group skips that the
+    first block re-emits and the last block adds in its MLP epilogue (the recomputed forward runs
+    the same deterministic kernels: logits and input gradients are bitwise equal)."""
+    kw = dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
+              attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=48, patch_size=4,
+              window_size=6, no_init_weights=True, volume_size=48)
+    plain = M.SwinFusion(**kw)
+    recipe.fill_params(plain)
+    ckpt = M.SwinFusion(use_checkpoint=True, **kw)
+    ckpt.load_state_dict(plain.state_dict())
+    A = torch.from_numpy(recipe.randn(8200, (2, 48, 48, 48)))
+    Bv = torch.from_numpy(recipe.randn(8201, (2, 48, 48, 48)))
+    tgt = torch.tensor([[1.0], [0.0]], device=device)
+    res = []
+    for m in (plain, ckpt):
+        _no_drop_path(m)
+        m = m.to(device)
+        ins = [t.to(device).requires_grad_(True) for t in (A, Bv)]
+        out = m(*ins)["binary_classification"]
+        torch.nn.functional.binary_cross_entropy_with_logits(out, tgt).backward()
+        torch.cuda.synchronize()
+        res.append((out.detach(), [t.grad for t in ins], {k: p.grad for k, p in m.named_parameters()}))
+    (o1, g1, p1), (o2, g2, p2) = res
+    assert torch.equal(o1, o2)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+    assert p1.keys() == p2.keys()
+    for k in p1:
+        if p1[k] is None:
+            assert p2[k] is None, k
+        else:   # the Swin-V2 head's dtau (logit_scale) sums in a different order: not bitwise
+            assert rel_err(p1[k], p2[k]) < 1e-5, k
