@@ -75,9 +75,11 @@ def parse():
     ap.add_argument("--size", type=int, default=None, help="volume side (voxels; default 96; c5: the fMRI side, 128)")
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1); the "
-                         "default for the launch-bound configs c2 and c4 (a few hundred small kernels per step)")
-    ap.add_argument("--eager", action="store_true", help="no hipGraph capture (c2 / c4 default to one at N = 1)")
+                    help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1 only); "
+                         "the default for the launch-bound configs c2 and c4 when --gpus is not given")
+    ap.add_argument("--eager", action="store_true",
+                    help="no hipGraph capture.  Implied whenever --gpus is given (so a 1/2/4/8-GPU curve compares "
+                         "eager steps at every N: the DDP step is not captured)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-size", type=int, default=36)
     return ap.parse_args()
@@ -328,19 +330,42 @@ def main():
     else:
         kw = model_kwargs(args.size)
         model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
-    graph = (args.graph or (args.config in ("c2", "c4") and not args.eager)) and world == 1
+    # hipGraph policy: explicit --graph (N = 1), or the c2 / c4 default when no --gpus was given; a
+    # --gpus run is eager at every N so the driver's 1 -> N curve compares like with like
+    if args.graph and world > 1:
+        raise SystemExit("bench.py: --graph captures a single-process step (N = 1); the DDP step runs eager")
+    graph = args.graph or (args.config in ("c2", "c4") and not args.eager and args.gpus is None and world == 1)
+    if graph:
+        # a captured step replays the host-drawn attention-dropout seed of the capture: refuse rather
+        # than train with one frozen mask (multihead_attention.py draws one per forward)
+        from multimodal_neuroimage_amd.modules.multihead_attention import MultiheadAttention
+        live = [n for n, m in model.named_modules()
+                if isinstance(m, MultiheadAttention) and m.training and float(m.attn_dropout) > 0]
+        if live:
+            raise SystemExit(f"bench.py: hipGraph capture with attention dropout in training ({live[0]}, ...) "
+                             "would freeze the dropout mask; run with --eager")
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank,
                               size_b=args.size * 3 // 4 if args.config == "c5" else None)
     inputs = (A,) if args.config == "c2" else (A, B)
     lossf = torch.nn.BCEWithLogitsLoss()
 
+    nvtx = torch.cuda.nvtx   # roctx on ROCm: the reference's NVTX points (trainer.py:373-430)
+
     def eager_step():
+        nvtx.range_push("training step")
         opt.zero_grad(set_to_none=True)
+        nvtx.range_push("forward")
         out = model(*inputs)["binary_classification"]
         loss = lossf(out, y)
+        nvtx.range_pop()
+        nvtx.range_push("backward")
         loss.backward()
+        nvtx.range_pop()
+        nvtx.range_push("optimize")
         opt.step()
+        nvtx.range_pop()
+        nvtx.range_pop()
         return loss
 
     step = eager_step
@@ -463,7 +488,8 @@ def main():
                                 f"on {(args.size // 8) ** 3}-token sequences in bf16 (front-end fp32)",
                        patch=8, patch_B=6, window=4, sequence=(args.size // 8) ** 3)}
         config = dict(workloads[args.config], global_batch=args.batch * world, per_gpu_batch=args.batch,
-                      volume=args.size, parallelism=f"dp{world}", checkpoint=args.checkpoint, graph=graph)
+                      volume=args.size, parallelism=f"dp{world}", checkpoint=args.checkpoint, graph=graph,
+                      step_mode="hipGraph replay of the whole step" if graph else "eager")
         metric = {"c2": METRIC_C2, "c5": METRIC_C5}.get(args.config, METRIC)
         line = dict(metric=metric, value=round(value, 4),
                     unit="volumes/s" if args.config == "c2" else "volume-pairs/s", n_gpus=world, steps=args.steps,

@@ -17,24 +17,12 @@ namespace blk {
 
 using namespace tt;
 
-#ifndef MMNI_LLF_U
-#define MMNI_LLF_U 4
-#endif
-#ifndef MMNI_LLB_U
-#define MMNI_LLB_U 2
-#endif
-constexpr int kLlfU = MMNI_LLF_U;   // tiles per step, ln_linear_fwd
-constexpr int kLlbU = MMNI_LLB_U;   // tiles per step, ln_linear_bwd (N = 12, 24)
+constexpr int kLlfU = 4;   // tiles per step, ln_linear_fwd
+constexpr int kLlbU = 2;   // tiles per step, ln_linear_bwd (N = 12, 24)
 // N = 36 keeps one tile per step: two would take it to 2 waves / SIMD (measured 270 vs 257 us)
 constexpr int llb_u(int n) { return n == 36 ? 1 : kLlbU; }
-#ifndef MMNI_LLF_LDS
-#define MMNI_LLF_LDS 1
-#endif
-constexpr bool kLlfLds = MMNI_LLF_LDS;   // ln_linear_fwd N > 12: outputs staged through LDS
-#ifndef MMNI_LLB_LDS
-#define MMNI_LLB_LDS 1
-#endif
-constexpr bool kLlbLds = MMNI_LLB_LDS;   // ln_linear_bwd N > 12: dy tiles staged through LDS
+// N > 12: ln_linear_fwd stages its outputs and ln_linear_bwd its dy tiles through LDS (N = 12
+// rows are 48 B: the accumulator layout already writes / reads them whole)
 
 struct TokArgs {
     int64_t rows;
@@ -81,8 +69,8 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
     }
 #pragma unroll
     for (int s = 0; s < CS; ++s) { gm[s] = a.gamma[4 * s + g]; bt[s] = a.beta[4 * s + g]; }
-    __shared__ __attribute__((aligned(16))) float ys_all[kLlfLds && N > 12 ? 4 * 16 * N : 4];
-    float* ys = ys_all + (kLlfLds && N > 12 ? (threadIdx.x >> 6) * 16 * N : 0);
+    __shared__ __attribute__((aligned(16))) float ys_all[N > 12 ? 4 * 16 * N : 4];
+    float* ys = ys_all + (N > 12 ? (threadIdx.x >> 6) * 16 * N : 0);
     const int64_t tiles = (a.rows + 15) / 16;
     // U consecutive tiles per step: their loads are issued together (one tile's 768 B per wave
     // in flight leaves the HBM latency exposed at this register budget)
@@ -99,7 +87,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
 #pragma unroll
             for (int s = 0; s < CS; ++s) xn[s] = fmaf((v[u][s] - mean) * rstd, gm[s], bt[s]);
             const bool ok = tl.token_ok(t0);
-            if constexpr (kLlfLds && N > 12) {
+            if constexpr (N > 12) {
                 // the tile's 16 x N outputs go through the wave's LDS slab, then out as contiguous
                 // 16-B stores (the accumulator layout writes each token row in N / 16 pieces)
 #pragma unroll
@@ -135,18 +123,12 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(TokArgs a) {
 // ------------------------------------------------------------------------------------
 // dx = LN_bwd(dy W) + dres;  dW = dy^T LN(x),  db = colsum dy,  dgamma, dbeta
 // ------------------------------------------------------------------------------------
-#ifndef MMNI_LLB_EARLY_RES
-#define MMNI_LLB_EARLY_RES 1
-#endif
-#ifndef MMNI_LLB36_WAVES
-#define MMNI_LLB36_WAVES 3
-#endif
 template <int N, int U>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N == 36 ? MMNI_LLB36_WAVES : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N == 36 ? 3 : 1)))
 void ln_linear_bwd_kernel(TokArgs a) {
     constexpr int NT = (N + 15) / 16;
     constexpr int NS = N / 4;   // k-steps over the N gradient columns
-    constexpr bool kEarlyRes = MMNI_LLB_EARLY_RES && N == 36;   // (N = 12 would drop to 3 waves / SIMD)
+    constexpr bool kEarlyRes = N == 36;   // (N = 12 would drop to 3 waves / SIMD)
     const int lane = threadIdx.x & 63;
     const Tile tl{a.rows, lane & 15, lane >> 4};
     const int t = tl.t, g = tl.g;
@@ -167,7 +149,7 @@ void ln_linear_bwd_kernel(TokArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) { dw[nt] = zero4(); db[nt] = 0.f; }
 
-    constexpr bool kDyLds = kLlbLds && N > 12;
+    constexpr bool kDyLds = N > 12;
     constexpr int DYV = (4 * N + 63) / 64;   // 16-B vectors per lane per dy tile
     __shared__ __attribute__((aligned(16))) float dys_all[kDyLds ? 4 * U * 16 * N : 4];
     float* dys = dys_all + (kDyLds ? (threadIdx.x >> 6) * U * 16 * N : 0);

@@ -150,21 +150,7 @@ __global__ __launch_bounds__(256) void conv3d_dx_kernel(ConvArgs a) {
 //   MODE 0 (forward):  out[v][o] = bias[o] + sum_t sum_i x[v + t - 1][i] * w[o][i][t], LeakyReLU
 //   MODE 1 (dx):       dx[v][i]  = sum_t sum_o dz[v + 1 - t][o] * w[o][i][t],
 //                      dz = dy * LeakyReLU'(y) computed once per halo row while staging.
-#ifndef MMNI_CONV_TAPW
-#define MMNI_CONV_TAPW 1   // k3 tile kernel: tap-inner loop with t-contiguous weight loads
-#endif
-#ifndef MMNI_CONV_PAIRW
-#define MMNI_CONV_PAIRW 1   // k3 tile kernel: channel pairs with 8-B aligned weight pairs
-#endif
-#ifndef MMNI_CONV_PAIRW_SB
-#define MMNI_CONV_PAIRW_SB 1
-#endif
-#ifndef MMNI_CONV_DW_BPC
-#define MMNI_CONV_DW_BPC 8   // dW kernel: persistent blocks per CU (each flushes its partials once)
-#endif
-#ifndef MMNI_CONV_TILE_ALL
-#define MMNI_CONV_TILE_ALL 1   // k3 forward: LDS tile for every channel pair (0: r05 selection)
-#endif
+constexpr int kDwBlocksPerCU = 8;   // dW kernel: persistent blocks per CU (each flushes its partials once)
 constexpr int kTX = 8, kTY = 8, kTZ = 4;
 constexpr int kHX = kTX + 2, kHY = kTY + 2, kHZ = kTZ + 2;
 
@@ -228,7 +214,6 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
     float acc[NO];
 #pragma unroll
     for (int o = 0; o < NO; ++o) acc[o] = (MODE == 0 && a.bias) ? a.bias[o] : 0.f;
-#if MMNI_CONV_TAPW
     // Tap-inner order: for one staged channel i, the 27 tap values come from LDS, and the weights of
     // one (i, o) pair are 27 consecutive floats (PyTorch layout, t fastest), fetched with a few wide
     // scalar loads.  The tap-outer order below issues one s_load_dword plus a 64-bit address add per
@@ -238,7 +223,7 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
     // starts at an even or odd float by a compile-time rule, so its taps go to v_pk_fma_f32 as
     // 8-B aligned pairs (aligned SGPR pairs, no realigning moves); the odd tap is a scalar FMA.
     // (forward only: the dx tile, 24 outputs per lane, measured slower paired: 2.77 vs 2.59 ms at 24 -> 12)
-    constexpr int IS = (MODE == 0 && NI % 2 == 0 && MMNI_CONV_PAIRW) ? 2 : 1;
+    constexpr int IS = (MODE == 0 && NI % 2 == 0) ? 2 : 1;
     typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll 1
     for (int i0 = 0; i0 < NI; i0 += IS) {
@@ -257,7 +242,7 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
                 const float* wp = a.w + (MODE == 0 ? (o * CIN + i) : (i * CIN + o)) * 27;
                 if (IS == 2) {
                     // one run's weights in SGPRs at a time (hoisting them all spills SGPRs to VGPR lanes)
-                    if (MMNI_CONV_PAIRW_SB) __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_sched_barrier(0);
                     // parity of the run start (i0 even): MODE 0 (o*CIN + si)*27, MODE 1 (si*CIN + o)*27
                     const int par = (MODE == 0 ? (o * CIN + si) : (si * CIN + o)) & 1;
                     f2 a2 = (f2){0.f, 0.f};
@@ -285,40 +270,6 @@ __global__ __launch_bounds__(256) void conv3d_k3_tile_kernel(ConvArgs a) {
             }
         }
     }
-#else
-    for (int t = 0; t < 27; ++t) {
-        const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
-        // forward reads x[v + k - 1] = halo[v_local + k]; dx reads dz[v + 1 - k] = halo[v_local + 2 - k]
-        const int hz = MODE == 0 ? tz + kz : tz + 2 - kz;
-        const int hy = MODE == 0 ? ty + ky : ty + 2 - ky;
-        const int hx = MODE == 0 ? tx + kx : tx + 2 - kx;
-        const float* r = halo + ((hz * kHY + hy) * kHX + hx) * RS;
-        float v[NI];
-        if constexpr (RS % 4 == 0) {
-#pragma unroll
-            for (int c = 0; c < NI; c += 4) {
-                const float4 q = *reinterpret_cast<const float4*>(r + c);
-                v[c] = q.x;
-                if (c + 1 < NI) v[c + 1] = q.y;
-                if (c + 2 < NI) v[c + 2] = q.z;
-                if (c + 3 < NI) v[c + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < NI; ++c) v[c] = r[c];
-        }
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-            float sacc = acc[o];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const float wv = MODE == 0 ? a.w[(o * CIN + i) * 27 + t] : a.w[(i * CIN + o) * 27 + t];
-                sacc = fmaf(v[i], wv, sacc);
-            }
-            acc[o] = sacc;
-        }
-    }
-#endif
     const int gx = bx * kTX + tx, gy = by * kTY + ty, gz = bz * kTZ + tz;
     if (gx >= a.W || gy >= a.H || gz >= a.D) return;
     const int64_t vox = (((int64_t)b * a.D + gz) * a.H + gy) * a.W + gx;
@@ -514,7 +465,7 @@ static int conv_fill(const mmni_conv3d_desc* d, ConvArgs& a) {
 }
 
 // dW tiling plan: output tile (TZ, TY, TX) shrunk until the LDS image (dz tile + input halo)
-// fits 64 KiB; persistent grid of at most kNumCU * MMNI_CONV_DW_BPC blocks.
+// fits 64 KiB; persistent grid of at most kNumCU * kDwBlocksPerCU blocks.
 static int dw_plan(ConvArgs& a, int& grid, size_t& lds) {
     const int CIN = a.Cin, COUT = a.Cout;
     int TZ = 4, TY = 4, TX = 16;
@@ -539,7 +490,7 @@ static int dw_plan(ConvArgs& a, int& grid, size_t& lds) {
     a.ntiles = a.B * a.ntz * a.nty * a.ntx;
     const int npairs = a.kd * a.kh * a.kw * CIN;
     MMNI_ARG_CHECK(npairs <= 1024, "conv3d_dw: k^3*Cin = %d exceeds 1024 pairs", npairs);
-    grid = a.ntiles < kNumCU * MMNI_CONV_DW_BPC ? a.ntiles : kNumCU * MMNI_CONV_DW_BPC;
+    grid = a.ntiles < kNumCU * kDwBlocksPerCU ? a.ntiles : kNumCU * kDwBlocksPerCU;
     // the group reduction of the MAXP 1 kernel ([G][npairs][COUT]) and the db reduction
     // ([COUT][256]) reuse the LDS image
     const int G = npairs <= 256 ? (256 / npairs > 0 ? 256 / npairs : 1) : 1;
@@ -552,9 +503,9 @@ static int dw_plan(ConvArgs& a, int& grid, size_t& lds) {
 
 template <int CIN, int COUT>
 static int conv_fwd_launch(ConvArgs& a, hipStream_t s) {
-    // measured at 96^3 (r05): the LDS tile wins for CIN <= 12 with >= 6 outputs, or CIN <= 3; the
-    // lane-per-voxel gather is faster for 24 -> 12 (tile LDS 67 KB: 2 blocks/CU) and 6 -> 3
-    if (is_k3_same(a) && (MMNI_CONV_TILE_ALL || (CIN <= 12 && COUT >= 6) || CIN <= 3)) {
+    // every k3 same-padding forward takes the LDS tile (tap-inner weights: faster than the lane-per-
+    // voxel gather at every channel pair since r10); other geometries (k = s = p) the gather
+    if (is_k3_same(a)) {
         MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(a.w) % 8 == 0, "conv3d_fwd: k3 weights must be 8-byte aligned");
         conv3d_k3_tile_kernel<CIN, COUT, 0><<<k3_tiles(a), 256, 0, s>>>(a);
         return launch_status("conv3d_fwd_k3");

@@ -228,19 +228,10 @@ __global__ __launch_bounds__(256) void mlp_fwd_kernel(MlpArgs a) {
 // ------------------------------------------------------------------------------------
 constexpr int kBwdWaves = 4;   // waves per block (LDS transpose slab per wave)
 
-#ifndef MMNI_MLP_BWD_WLDS
-#define MMNI_MLP_BWD_WLDS 1
-#endif
-constexpr bool kWLds = MMNI_MLP_BWD_WLDS;
-#ifndef MMNI_LN_MLP_BWD_OCC
-#define MMNI_LN_MLP_BWD_OCC 3
-#endif
-#ifndef MMNI_MLP_BWD_OCC
-#define MMNI_MLP_BWD_OCC 3   // min waves per SIMD (caps VGPRs at 168)
-#endif
+constexpr int kMlpBwdOcc = 3;   // min waves per SIMD (caps VGPRs at 168)
 // (the LN variant carries ~20 more live values: 2 waves per SIMD, no spills)
 template <bool LN>
-__global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) void mlp_bwd_kernel(MlpArgs a) {
+__global__ __launch_bounds__(256, kMlpBwdOcc) void mlp_bwd_kernel(MlpArgs a) {
     __shared__ float tr[kBwdWaves][2][16][H + 4];   // per wave: g and dpre as [token][hidden]
     const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
     const int wib = threadIdx.x >> 6;
@@ -249,10 +240,10 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
     const TileIO io{a.rows, li, lg};
     float w1a[HT][CS], w2ta[HT][CS], w1ta[HT][4];
     f4 b1c[HT];
-    // MMNI_MLP_BWD_WLDS: the 42 per-lane weight values live in LDS ([value][lane]: conflict-free)
-    // and are re-read per tile, which frees their VGPRs for a third wave per SIMD
+    // the 42 per-lane weight values live in LDS ([value][lane]: conflict-free) and are re-read per
+    // tile, which frees their VGPRs for a third wave per SIMD
     constexpr int NWV = HT * (2 * CS + 8);
-    __shared__ float wv_s[kWLds ? NWV * 64 : 1];
+    __shared__ float wv_s[NWV * 64];
     auto wload = [&]() {
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
@@ -269,21 +260,17 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
         }
     };
     auto wslot = [&](int ht, int k) -> float& { return wv_s[(ht * (2 * CS + 8) + k) * 64 + lane]; };
-    if constexpr (kWLds) {
-        if (wib == 0) {
-            wload();
-#pragma unroll
-            for (int ht = 0; ht < HT; ++ht) {
-#pragma unroll
-                for (int s = 0; s < CS; ++s) { wslot(ht, s) = w1a[ht][s]; wslot(ht, CS + s) = w2ta[ht][s]; }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) { wslot(ht, 2 * CS + i) = w1ta[ht][i]; wslot(ht, 2 * CS + 4 + i) = b1c[ht][i]; }
-            }
-        }
-        __syncthreads();
-    } else {
+    if (wib == 0) {
         wload();
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+            for (int s = 0; s < CS; ++s) { wslot(ht, s) = w1a[ht][s]; wslot(ht, CS + s) = w2ta[ht][s]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { wslot(ht, 2 * CS + i) = w1ta[ht][i]; wslot(ht, 2 * CS + 4 + i) = b1c[ht][i]; }
+        }
     }
+    __syncthreads();
     f4 dw1[HT], dw2[HT];   // dW1 tile ht: rows hid, cols c;  dW2 tile ht: rows o, cols hid
     f4 db1[HT];            // per-lane partial column sums of dpre (rows hid, this lane's tokens)
     float db2 = 0.f;       // per-lane partial of dy[., o = li]
@@ -311,28 +298,23 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
     const int64_t tiles = (a.rows + 15) / 16;
     for (int64_t tile = wave; tile < tiles; tile += nwaves) {
         const int64_t t0 = tile * 16;
-        if constexpr (kWLds) {
-            asm volatile("" ::: "memory");   // keep the weight reads in the loop (not hoisted)
+        asm volatile("" ::: "memory");   // keep the weight reads in the loop (not hoisted)
 #pragma unroll
-            for (int ht = 0; ht < HT; ++ht) {
+        for (int ht = 0; ht < HT; ++ht) {
 #pragma unroll
-                for (int s = 0; s < CS; ++s) { w1a[ht][s] = wslot(ht, s); w2ta[ht][s] = wslot(ht, CS + s); }
+            for (int s = 0; s < CS; ++s) { w1a[ht][s] = wslot(ht, s); w2ta[ht][s] = wslot(ht, CS + s); }
 #pragma unroll
-                for (int i = 0; i < 4; ++i) { w1ta[ht][i] = wslot(ht, 2 * CS + i); b1c[ht][i] = wslot(ht, 2 * CS + 4 + i); }
-            }
+            for (int i = 0; i < 4; ++i) { w1ta[ht][i] = wslot(ht, 2 * CS + i); b1c[ht][i] = wslot(ht, 2 * CS + 4 + i); }
         }
         float xb[CS], dyb[CS], xa[4], dya[4];
         io.load_fm(a.x, t0, xb);
         io.load_fm(a.dy, t0, dyb);
         io.load_tm(a.x, t0, xa);
         io.load_tm(a.dy, t0, dya);
-#ifndef MMNI_MLP_BWD_EARLY
-#define MMNI_MLP_BWD_EARLY 1
-#endif
         // LN variant: the chunk-layout x and dy rows of the LN backward / residual gradient load
         // with the tile's operands (after the MFMAs their latency was exposed once per tile)
         f4 xc_e = (f4){0.f, 0.f, 0.f, 0.f}, dyr_e = xc_e;
-        if constexpr (LN && MMNI_MLP_BWD_EARLY) {
+        if constexpr (LN) {
             if (io.row_ok(t0)) {
                 const int64_t roff = (t0 + li) * C + 4 * lg;
                 xc_e = *reinterpret_cast<const f4*>(a.x + roff);
@@ -388,14 +370,13 @@ __global__ __launch_bounds__(256, LN ? MMNI_LN_MLP_BWD_OCC : MMNI_MLP_BWD_OCC) v
             const bool ok = io.row_ok(t0);
             const int64_t roff = (t0 + li) * C + 4 * lg;
             const f4 dxn = dxo[0] + dxo[1] + dxo[2];
-            const f4 xc = MMNI_MLP_BWD_EARLY ? xc_e : ok ? *reinterpret_cast<const f4*>(a.x + roff) : (f4){0.f, 0.f, 0.f, 0.f};
+            const f4 xc = xc_e;
             const f4 xh = ok ? (xc - mean) * rstd : (f4){0.f, 0.f, 0.f, 0.f};
             const f4 gd = dxn * gm4;
             const float s1 = sum_groups(gd[0] + gd[1] + gd[2] + gd[3]) * (1.0f / C);
             const float s2 = sum_groups(gd[0] * xh[0] + gd[1] * xh[1] + gd[2] * xh[2] + gd[3] * xh[3]) * (1.0f / C);
             f4 dxv = (gd - s1 - xh * s2) * rstd;
-            if (MMNI_MLP_BWD_EARLY) dxv += dyr_e;
-            else if (a.res_x && ok) dxv += *reinterpret_cast<const f4*>(a.dy + roff);
+            dxv += dyr_e;
             if (ok) *reinterpret_cast<f4*>(a.dx + roff) = dxv;
             dgm += dxn * xh;
             dbt += dxn;

@@ -208,9 +208,6 @@ __global__ __launch_bounds__(256) void token_linear_kernel(TLinArgs a) {
 // per wave step on the f32 MFMA in the accumulator-chunk layout of tokentile.h (as blockops'
 // linear_bwd), y^T = W x^T.  No LDS staging and no block barriers: the LDS-tiled path above
 // moved the same bytes at ~3.7 TB/s.
-#ifndef MMNI_TLIN12_MFMA
-#define MMNI_TLIN12_MFMA 1
-#endif
 __global__ __launch_bounds__(256) void linear12_fwd_kernel(TLinArgs a) {
     using namespace tt;
     const int lane = threadIdx.x & 63;
@@ -268,7 +265,7 @@ extern "C" int mmni_token_linear(const mmni_tlin_desc* d, const float* x, const 
     a.x = x; a.w = w; a.bias = bias; a.aux = aux; a.w2 = w2; a.b2 = b2; a.res = residual; a.y = y;
     const int64_t blocks = (d->rows + 255) / 256;
     hipStream_t s = (hipStream_t)stream;
-    if (MMNI_TLIN12_MFMA && d->K == 12 && d->N == 12 && d->epi == 0 && d->ldx == 12 && d->ldy == 12) {
+    if (d->K == 12 && d->N == 12 && d->epi == 0 && d->ldx == 12 && d->ldy == 12) {
         static const int resident =
             tt::resident_blocks(reinterpret_cast<const void*>(&linear12_fwd_kernel), 256, 0);
         const int64_t need = (d->rows + 63) / 64;   // 4 waves x 16-token tiles per block

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     float* tab_s = reinterpret_cast<float*>(meta_s + T); // [Tsz][NH] (log2 domain)
     unsigned long long* dtab_s =                          // [Tsz][NH] grad, 64-bit fixed point
         reinterpret_cast<unsigned long long*>(tab_s + ((g.Tsz * NH + 1) & ~1));
-    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * NH);   // [NH]
+    float* dtau_s = reinterpret_cast<float*>(dtab_s + g.Tsz * NH);   // [kMaxWaves][NH]
 
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -274,7 +274,6 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
         tab_s[e] = a.table[e] * kLog2e;
         dtab_s[e] = 0ull;
     }
-    if (tid < NH) dtau_s[tid] = 0.f;
     const float ymul = exp2f((float)fix_exponent(a.maxbits, HD));
     float dtr[NH];
 #pragma unroll
@@ -494,13 +493,14 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
         __syncthreads();
     }
 
-    // ---- dtau: wave reduce then one LDS atomic per wave; flush LDS accumulators
+    // ---- dtau: fixed butterfly per wave into its LDS slot, waves summed in order into this
+    // block's partial row; flush the (exact, order-free) fixed-point table-gradient sums
     if (KIND == 1) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
             float v = dtr[h];
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if (lane == 0) atomicAdd(&dtau_s[h], v);
+            if (lane == 0) dtau_s[(tid >> 6) * NH + h] = v;
         }
     }
     __syncthreads();
@@ -510,7 +510,9 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     }
     if (KIND == 1 && tid < NH) {
         // dtau = sum ds * (q-hat . k-hat);  dot was taken against tau*log2e*q-hat
-        atomicAdd(&a.dtau[tid], dtau_s[tid] / (a.tau[tid] * kLog2e));
+        float v = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += dtau_s[w * NH + tid];
+        a.dtau_part[(size_t)blockIdx.x * NH + tid] = v / (a.tau[tid] * kLog2e);
     }
 }
 
@@ -605,22 +607,22 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
     if (packed)
         return T * (2 * C + 2 * NH) * 4 + T * 8 + (size_t)Tsz * (NH == 2 ? 2 : (NH + 3) & ~3) * 4 +
                (size_t)Tsz * (NH + kDtabPad) * 8 +
-               (size_t)NH * 4;
+               (size_t)kMaxWaves * NH * 4;
     const size_t tab = (size_t)((Tsz * NH + 1) & ~1) * 4;
-    return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)NH * 4;
+    return T * (2 * C + 2 * NH) * 4 + T * 8 + tab + (size_t)Tsz * NH * 8 + (size_t)kMaxWaves * NH * 4;
 }
 
 // qpl: queries per lane (2 for wattn_fwd_pk2_kernel, forward only): a window occupies N / qpl x KS lanes.
 static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
-    const int chunk = packed ? (qpl >= 2 ? MMNI_PK2_CHUNK : kPkChunk) : CH;
+    const int chunk = packed ? (qpl >= 2 ? kPk2Chunk : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl >= 2 ? MMNI_PK2_KS : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    int KS = qpl >= 2 ? kPk2Ks : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (R * KS);
-    if (qpl == 2 && !bwd && WPB > MMNI_PK2_FWD_WPB) WPB = MMNI_PK2_FWD_WPB;
+    if (qpl == 2 && !bwd && WPB > kPk2FwdWpb) WPB = kPk2FwdWpb;
     if (WPB < 1) WPB = 1;
     const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
@@ -759,7 +761,9 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
 extern "C" size_t mmni_wattn_bwd_workspace_bytes(const mmni_wattn_desc* d) {
     WGeom g;
     if (make_geom(d, g)) return 0;
-    const size_t fixed = (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16;   // + the two absmax words
+    // fixed-point table gradient + the two absmax words + the dtau partial rows (kind 1)
+    const size_t fixed = (size_t)g.Tsz * d->heads * sizeof(unsigned long long) + 16 +
+                         (size_t)kMaxBwdBlocks * d->heads * sizeof(float);
     if (d->heads > 0 && wattn_bc_supported(g, d->C, d->heads, d->kind)) {
         const size_t b = wattn_bc_workspace_bytes(g, d->heads);
         return b > fixed ? b : fixed;
@@ -812,6 +816,8 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     if (rc) return rc;
     const int ntab = a.g.Tsz * d->heads;
     a.maxbits = reinterpret_cast<unsigned int*>(a.dtab_fix + ntab);
+    a.dtau_part = reinterpret_cast<float*>(a.maxbits + 4);
+    MMNI_ARG_CHECK(cfg.grid <= kMaxBwdBlocks, "wattn_bwd: grid %d exceeds the dtau partial rows", cfg.grid);
     hipError_t e = hipMemsetAsync(workspace, 0, (size_t)ntab * 8 + 16, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd memset: %s", hipGetErrorString(e)); return (int)e; }
     const long long T = (long long)a.g.nwin * a.g.N;   // tokens
@@ -832,7 +838,15 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
     wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD,
                                                                                      a.fix_shift, dtable, ntab);
-    return launch_status("wattn_dtable_convert");
+    rc = launch_status("wattn_dtable_convert");
+    if (rc || d->kind != 1) return rc;
+    ColSegs segs{};   // dtau += the fixed-order column sums of the blocks' partial rows
+    segs.n = 1;
+    segs.end[0] = d->heads;
+    segs.dst[0] = dtau;
+    segs.accumulate = 1;
+    column_sum_segs(a.dtau_part, cfg.grid, d->heads, segs, (hipStream_t)stream);
+    return launch_status("wattn_dtau_sum");
 }
 
 extern "C" int mmni_window_rows(const mmni_wattn_desc* d, int32_t* rows, void* stream) {

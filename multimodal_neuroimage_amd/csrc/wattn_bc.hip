@@ -6,8 +6,7 @@
 //   forward   wattn_fwd_bcs_kernel  lane = query pair (t, t + N/2); the wave walks the keys in
 //                                   lock step, each key record an LDS broadcast read; online softmax;
 //                                   a 4-wave workgroup streams the query pairs of a list of windows
-//                                   (all lanes busy).  wattn_fwd_bc_kernel: one (window, head pair)
-//                                   per 2-wave workgroup (108 of 128 lanes)
+//                                   (all lanes busy)
 //   backward  wattn_bwd_q4m_kernel  lane = query quad (y + 3, z + 3 partners); the wave walks the
 //                                   54 key quads; per step p and ds of 16 (query, key) pairs give
 //                                   dq (registers), the bias-table gradient (private LDS image) and
@@ -69,24 +68,6 @@ __device__ __forceinline__ void store_row_nat(float* dst, const Row& r, float sc
     *reinterpret_cast<float4*>(dst) =
         make_float4(r.x[0].x * scale, r.x[1].x * scale, r.x[0].y * scale, r.x[1].y * scale);
 }
-
-// (window, head pair) items: the NHG head-pair workgroups of a window sit 8 block indices apart,
-// i.e. on one XCD (blocks are dealt round-robin over the 8 XCDs), so a window's rows are fetched
-// from HBM once into that XCD's L2.  The grid is a multiple of 8 * NHG.
-struct Items {
-    int hp, first, stride;
-};
-
-__device__ __forceinline__ Items items(int NHG) {
-    Items it;
-    const int xslot = blockIdx.x >> 3;
-    it.hp = xslot % NHG;
-    it.first = (xslot / NHG) * 8 + (blockIdx.x & 7);
-    it.stride = gridDim.x / NHG;
-    return it;
-}
-
-constexpr int kThreads = 128;   // two waves: N / 2 <= 128 row pairs
 
 // Lane -> row-pair map of 6^3 windows.  A lane's table entries at one step are code(t) + const,
 // and 8-byte LDS accesses conflict on (code mod 32) within 32-lane halves (ds_read_b64) and on
@@ -262,113 +243,6 @@ __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[
                 if (BOUNDED) __builtin_amdgcn_sched_barrier(0);
             }
         }
-    }
-}
-
-template <int WD, int WH, int WW>
-__global__ __launch_bounds__(bc::kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-void wattn_fwd_bc_kernel(WAArgs a) {
-    using Wn = bc::Win<WD, WH, WW>;
-    constexpr int H = Wn::H, TSZ = Wn::TSZ;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const WGeom& g = a.g;
-    const int NHG = a.hsplit, NHT = 2 * NHG;
-    float* tab_s = smem;                 // [TSZ] f2: bias * log2e of the head pair
-    float* kv_s = tab_s + bc::align4(TSZ * 2);   // [H][8] f2: key records as in pass A
-    float* red = kv_s + H * 16;          // [2 waves][2 heads] max |bias|, then [2][2] max |k|^2
-    const bc::Items it = bc::items(NHG);
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const bool lane_ok = tid < H;
-    const int t = lane_ok ? (int)bc::kPerm666[tid] : 0;
-    float tabs = 0.f;   // this thread's entries all belong to head tid & 1 (the stride is even)
-    for (int e = tid; e < TSZ * 2; e += blockDim.x) {
-        const float x = a.table[(e >> 1) * NHT + 2 * it.hp + (e & 1)] * kLog2e;
-        tab_s[e] = x;
-        tabs = fmaxf(tabs, fabsf(x));
-    }
-    for (int off = 2; off < 64; off <<= 1) tabs = fmaxf(tabs, __shfl_xor(tabs, off));
-    if ((tid & 63) < 2) red[wave * 2 + (tid & 1)] = tabs;
-    __syncthreads();
-    const f2 tmax = (f2){fmaxf(red[0], red[2]), fmaxf(red[1], red[3])};
-    const int coff = it.hp * 4;
-    const f2 qscale = bc::splat(a.scale * kLog2e);
-    float vabs = 0.f;
-    for (int w = it.first; w < g.nwin; w += it.stride) {
-        __syncthreads();   // previous window's K/V reads done (and the table staged, first time)
-        Row q[2], o[2];
-        f2 m[2], l[2];
-        int cq = 0, rq[2] = {0, 0};
-        int64_t row[2] = {0, 0};
-        const bc::Regions reg = bc::window_regions(g, w);
-        f2 kn = bc::splat(0.f);   // max |k|^2 per head over this lane's two keys
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int tt = t + u * H;
-                const TokenInfo ti = token_info(g, w, tt);
-                row[u] = ti.row;
-                rq[u] = bc::region_code(reg, tt / (WW * WH), (tt / WW) % WH, tt % WW);
-                if (u == 0) cq = ti.code + Wn::OFF;
-                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
-                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
-                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
-                q[u].x[0] *= qscale;
-                q[u].x[1] *= qscale;
-                kn = (f2){fmaxf(kn.x, kr.x * kr.x + kr.y * kr.y), fmaxf(kn.y, kr.z * kr.z + kr.w * kr.w)};
-                vabs = fmaxf(vabs, fmaxf(fmaxf(fabsf(vr.x), fabsf(vr.y)), fmaxf(fabsf(vr.z), fabsf(vr.w))));
-                f2* kv2 = reinterpret_cast<f2*>(kv_s) + t * 8 + u * 4;   // key record t
-                kv2[0] = (f2){kr.x, kr.z};
-                kv2[1] = (f2){kr.y, kr.w};
-                kv2[2] = (f2){vr.x, vr.z};
-                kv2[3] = (f2){vr.y, vr.w};
-                l[u] = bc::splat(0.f);
-                o[u].x[0] = o[u].x[1] = bc::splat(0.f);
-            }
-        }
-        for (int off = 1; off < 64; off <<= 1)
-            kn = (f2){fmaxf(kn.x, __shfl_xor(kn.x, off)), fmaxf(kn.y, __shfl_xor(kn.y, off))};
-        if ((tid & 63) == 0) {
-            red[4 + wave * 2] = kn.x;
-            red[5 + wave * 2] = kn.y;
-        }
-        __syncthreads();
-        // per wave: every row within the bound (the previous window's reads of red[4..7] finished
-        // before this window's first barrier)
-        const f2 kmax2 = (f2){fmaxf(red[4], red[6]), fmaxf(red[5], red[7])};
-        bool rows_ok = true;
-        if (lane_ok) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const f2 qn = bc::pfma(q[u].x[0], q[u].x[0], q[u].x[1] * q[u].x[1]);
-                const f2 qk = qn * kmax2;
-                rows_ok = rows_ok && __builtin_sqrtf(qk.x) + tmax.x <= kFwdBound &&
-                          __builtin_sqrtf(qk.y) + tmax.y <= kFwdBound;
-            }
-        }
-        const bool bounded = __all(rows_ok);
-        if (lane_ok) {
-            if (bounded) {
-                if (reg.masked) fwd_loop<WD, WH, WW, true, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
-                else fwd_loop<WD, WH, WW, false, true>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
-            } else {
-                if (reg.masked) fwd_loop<WD, WH, WW, true, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
-                else fwd_loop<WD, WH, WW, false, false>(q, m, l, o, cq, rq, reg, tab_s, kv_s);
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const f2 inv = (f2){1.0f / l[u].x, 1.0f / l[u].y};
-                Row r;
-                r.x[0] = o[u].x[0] * inv;
-                r.x[1] = o[u].x[1] * inv;
-                bc::store_row_nat(a.out + row[u] * a.os + coff, r, 1.0f);
-                a.lse[row[u] * NHT + 2 * it.hp] = (m[u].x + fast_log2(l[u].x)) * kLn2;
-                a.lse[row[u] * NHT + 2 * it.hp + 1] = (m[u].y + fast_log2(l[u].y)) * kLn2;
-            }
-        }
-    }
-    if (a.vmax != nullptr) {
-        for (int off = 32; off > 0; off >>= 1) vabs = fmaxf(vabs, __shfl_xor(vabs, off));
-        if ((tid & 63) == 0) atomicMax(a.vmax, __float_as_uint(vabs));
     }
 }
 
@@ -707,11 +581,8 @@ constexpr int REC = 108 * 64;          // records of one window (pair t: keys t,
 constexpr int SLOT = REC + 16;         // ring stride: consecutive slots 16 B apart modulo 128 B
 }  // namespace fs
 
-#ifndef MMNI_FS_WAVES
-#define MMNI_FS_WAVES 4
-#endif
 template <int WD, int WH, int WW>
-__global__ __launch_bounds__(fs::WAVES * 64) __attribute__((amdgpu_waves_per_eu(MMNI_FS_WAVES)))
+__global__ __launch_bounds__(fs::WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
 void wattn_fwd_bcs_kernel(WAArgs a) {
     using Wn = bc::Win<WD, WH, WW>;
     constexpr int H = Wn::H, TSZ = Wn::TSZ;
@@ -851,17 +722,6 @@ bool wattn_bc_supported(const WGeom& g, int C, int heads, int kind) {
 }
 
 
-// persistent grid: resident workgroups per CU from the LDS footprint and the register budget
-// (waves_per_eu of the kernel: 2-wave workgroups, 4 SIMDs), a multiple of 8 * NHG
-static int bc_blocks(size_t lds, int NHG, int waves_per_eu) {
-    int per_cu = (int)((160 * 1024) / lds);
-    if (per_cu > 2 * waves_per_eu) per_cu = 2 * waves_per_eu;
-    if (per_cu < 1) per_cu = 1;
-    int grid = kNumCU * per_cu;
-    grid -= grid % (8 * NHG);
-    return grid < 8 * NHG ? 8 * NHG : grid;
-}
-
 // merged backward: per_cu resident 4-wave workgroups per CU (2 by LDS), a multiple of 8 with every
 // head pair served
 static int q4_blocks(int per_cu, int NHG) {
@@ -885,11 +745,6 @@ static int set_lds_limit(const void* fn, size_t bytes) {
     return 0;
 }
 
-static size_t bcF_lds() { return (size_t)bc::align4(bc::Win<6, 6, 6>::TSZ * 2) * 4 + (size_t)8 * bc::Win<6, 6, 6>::H * 8 + 8 * 4; }
-
-#ifndef MMNI_FWD_STREAM
-#define MMNI_FWD_STREAM 1   // forward with streaming lanes (all 256 lanes of a workgroup busy)
-#endif
 
 int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     const WGeom& g = a.g;
@@ -897,20 +752,13 @@ int wattn_bc_forward(WAArgs& a, int heads, hipStream_t s) {
     MMNI_ARG_CHECK(g.wd == 6 && g.wh == 6 && g.ww == 6 && g.Tsz == kTsz666, "wattn_fwd (broadcast): compiled for 6^3 windows");
     const int NHG = heads / 2;
     a.hsplit = NHG;
-    if (MMNI_FWD_STREAM) {
-        const size_t lds = (size_t)bc::align4(kTsz666 * 2) * 4 + (size_t)fs::RING * fs::SLOT +
-                           (size_t)(2 * fs::WAVES + 4 * fs::RING) * 4;
-        int per = (MMNI_FS_WAVES * kNumCU) / (8 * NHG);   // 4-wave workgroups per CU (one per wave/SIMD)
-        if (per < 1) per = 1;
-        wattn_fwd_bcs_kernel<6, 6, 6><<<8 * NHG * per, fs::WAVES * 64, lds, s>>>(a);
-        return launch_status("wattn_fwd_bcs");
-    }
-    const size_t lds = bcF_lds();
-    const int grid = bc_blocks(lds, NHG, 4);
-    int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_fwd_bc_kernel<6, 6, 6>), lds);
-    if (rc) return rc;
-    wattn_fwd_bc_kernel<6, 6, 6><<<grid, bc::kThreads, lds, s>>>(a);
-    return launch_status("wattn_fwd_bc");
+    // forward with streaming lanes (all 256 lanes of a workgroup busy), 4 waves per SIMD
+    const size_t lds = (size_t)bc::align4(kTsz666 * 2) * 4 + (size_t)fs::RING * fs::SLOT +
+                       (size_t)(2 * fs::WAVES + 4 * fs::RING) * 4;
+    int per = (4 * kNumCU) / (8 * NHG);   // 4-wave workgroups per CU (one per wave/SIMD)
+    if (per < 1) per = 1;
+    wattn_fwd_bcs_kernel<6, 6, 6><<<8 * NHG * per, fs::WAVES * 64, lds, s>>>(a);
+    return launch_status("wattn_fwd_bcs");
 }
 
 int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipStream_t s) {

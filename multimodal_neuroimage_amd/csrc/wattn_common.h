@@ -75,32 +75,23 @@ struct WAArgs {
     int fix_shift;                  // bits the fixed-point scale is lowered by (0: every kernel here)
     unsigned int* vmax;             // forward (packed kernels): running max|v| (float bits), or null
     int hsplit;                     // head groups per window (blocks split the heads; row-broadcast bwd: head pairs)
+    float* dtau_part;               // kind 1 backward: one dtau partial row (NH floats) per block (workspace)
 };
+
+// kind 1 backward: the per-wave dtau sums land in LDS slots (no atomics) and each block writes
+// one fixed-order partial row; a fixed-order column sum adds the rows into dtau (deterministic).
+constexpr int kMaxWaves = 16;                   // 1024-thread blocks
+constexpr int kMaxBwdBlocks = 8 * 256;          // resident-grid cap of the generic backward (plan())
 
 constexpr float kMask2 = -100.0f * kLog2e;  // -100 shift mask in the log2 domain
 constexpr float kNormEps = 1e-12f;          // F.normalize eps (swin_v2_module.py:153)
 constexpr int CH = 4;                       // keys per online-softmax chunk (generic kernels)
-#ifndef MMNI_PK_CHUNK
-#define MMNI_PK_CHUNK 6
-#endif
-#ifndef MMNI_DTAB_PAD
-#define MMNI_DTAB_PAD 1
-#endif
-#ifndef MMNI_TAB_SWZ
-#define MMNI_TAB_SWZ 1
-#endif
-#ifndef MMNI_PK2_CHUNK
-#define MMNI_PK2_CHUNK 3      // keys per online-softmax chunk of the two-query forward
-#endif
-#ifndef MMNI_PK2_KS
-#define MMNI_PK2_KS 1         // key slices (lanes per query pair) of the two-query forward
-#endif
-#ifndef MMNI_PK2_FWD_WPB
-#define MMNI_PK2_FWD_WPB 2    // windows per block of the two-query forward: two blocks share a CU
-#endif
-constexpr int kDtabPad = MMNI_DTAB_PAD;   // packed bwd: table-gradient row stride NH + pad (u64)
-constexpr int kTabSwz = MMNI_TAB_SWZ;     // packed bwd: float4 chunks of table row r XOR-ed with (r >> 3)
-constexpr int kPkChunk = MMNI_PK_CHUNK;     // keys per online-softmax chunk (packed kernels)
+constexpr int kDtabPad = 1;   // packed bwd: table-gradient row stride NH + pad (u64)
+constexpr int kTabSwz = 1;     // packed bwd: float4 chunks of table row r XOR-ed with (r >> 3)
+constexpr int kPkChunk = 6;     // keys per online-softmax chunk (packed kernels)
+constexpr int kPk2Chunk = 3;    // keys per online-softmax chunk of the two-query forward
+constexpr int kPk2Ks = 1;       // key slices (lanes per query pair) of the two-query forward
+constexpr int kPk2FwdWpb = 2;   // windows per block of the two-query forward: two blocks share a CU
 
 // Packed head_dim-2 kernels (wattn_pk.hip): fills kf/kb/maxt and returns 1 when C is covered.
 int wattn_pk_kernels(int C, int kind, int N, void*& kf, void*& kb, int& maxt_f, int& maxt_b, int& qpl_f);

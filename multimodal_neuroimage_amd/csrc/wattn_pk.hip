@@ -253,7 +253,7 @@ __global__ __launch_bounds__(MAXT, C == 12 ? 4 : 1) void wattn_fwd_pk_kernel(WAA
 // two queries (LDS instructions per query-key pair 8.5 -> 5).  Lanes per window: N/2 x KS.
 template <int C, int KIND, int MAXT, int QPL = 2>
 __global__ __launch_bounds__(MAXT) void wattn_fwd_pk2_kernel(WAArgs a) {
-    constexpr int HD = 2, NH = C / HD, NP = NH / 2, CK = MMNI_PK2_CHUNK;
+    constexpr int HD = 2, NH = C / HD, NP = NH / 2, CK = kPk2Chunk;
     static_assert(NH % 2 == 0, "head pairs");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const WGeom& g = a.g;
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
     int2* meta_s = reinterpret_cast<int2*>(rs_s + (size_t)T * 2 * NH);
     float* tab_s = reinterpret_cast<float*>(meta_s + T);  // [Tsz][NHP], log2-domain bias
     dt_t* dtab_s = reinterpret_cast<dt_t*>(tab_s + (size_t)g.Tsz * NHP);
-    float* dtau_s = reinterpret_cast<float*>(dtab_s + (size_t)g.Tsz * DS);
+    float* dtau_s = reinterpret_cast<float*>(dtab_s + (size_t)g.Tsz * DS);   // [kMaxWaves][NH]
 
     const int tid = threadIdx.x;
     const int r = tid / KS, p = tid - r * KS;
@@ -547,7 +547,6 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
         tab_s[tab_pos<NHP>(row, h)] = h < NH ? a.table[row * NH + h] * kLog2e : 0.f;
     }
     for (int e = tid; e < g.Tsz * DS; e += blockDim.x) dtab_s[e] = 0;
-    if (tid < NH) dtau_s[tid] = 0.f;
     const int fexp = fix_exponent(a.maxbits, HD) - a.fix_shift;
     const float fs = exp2f((float)fexp);       // 2^S
     const float ifs = exp2f((float)-fexp);     // 2^-S (exact)
@@ -833,8 +832,8 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
             f2 v = dtr[P];
             for (int o = 32; o > 0; o >>= 1) v += shfl2(v, o);
             if (lane == 0) {
-                atomicAdd(&dtau_s[2 * P], v.x);
-                atomicAdd(&dtau_s[2 * P + 1], v.y);
+                dtau_s[(tid >> 6) * NH + 2 * P] = v.x;
+                dtau_s[(tid >> 6) * NH + 2 * P + 1] = v.y;
             }
         }
     }
@@ -843,7 +842,11 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_pk_kernel(WAArgs a) {
         const dt_t v = dtab_s[(e / NH) * DS + e % NH];
         if (v != 0) atomicAdd(&a.dtab_fix[e], v);
     }
-    if (KIND == 1 && tid < NH) atomicAdd(&a.dtau[tid], dtau_s[tid] * ifs / (a.tau[tid] * kLog2e));
+    if (KIND == 1 && tid < NH) {   // this block's partial row, waves summed in a fixed order
+        float v = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += dtau_s[w * NH + tid];
+        a.dtau_part[(size_t)blockIdx.x * NH + tid] = v * ifs / (a.tau[tid] * kLog2e);
+    }
 }
 
 // ------------------------------------------------------------------------------------

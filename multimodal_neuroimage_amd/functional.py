@@ -354,16 +354,33 @@ class _MhaMeanProbs(torch.autograd.Function):
         hd = E // heads
         qh = q.float().reshape(Tq, B, heads, hd).permute(1, 2, 0, 3)     # (B, h, Tq, d)
         kh = k.float().reshape(Tk, B, heads, hd).permute(1, 2, 0, 3)     # (B, h, Tk, d)
-        s = torch.matmul(qh, kh.transpose(-1, -2)) * scale
-        if diag > 0:
-            s = s + torch.triu(torch.full((Tq, Tk), float("-inf"), device=q.device), diag)
-        p = torch.exp(s - lse.unsqueeze(-1))                              # the forward's softmax
-        dp = (dw.float() / heads).unsqueeze(1).expand(B, heads, Tq, Tk)
-        if dropout > 0:
-            dp = dp * mha_dropout_mask(Tq, Tk, B, heads, dropout, seed, q.device, diag)
-        ds = p * (dp - (dp * p).sum(-1, keepdim=True))
-        dq = (torch.matmul(ds, kh) * scale).permute(2, 0, 1, 3).reshape(Tq, B, E)
-        dk = (torch.matmul(ds.transpose(-1, -2), qh) * scale).permute(2, 0, 1, 3).reshape(Tk, B, E)
+        dq = torch.empty((B, heads, Tq, hd), device=q.device, dtype=torch.float32)
+        dk = torch.empty((B, heads, Tk, hd), device=q.device, dtype=torch.float32)
+        causal = (torch.triu(torch.full((Tq, Tk), float("-inf"), device=q.device), diag) if diag > 0 else None)
+        # the dense (Tq, Tk) rebuild runs over (batch, head-chunk) slices sized to ~256 MB per
+        # tensor, so C5-sized calls (8 x 12 x 4096^2) do not materialise 6.4 GB tensors
+        hc = max(1, min(heads, (64 << 20) // max(1, Tq * Tk)))
+        # (dropout: the kernels' mask is generated once for the whole call; only this rarely used
+        # path, back-propagation through the returned weights with dropout on, holds it whole)
+        dmask = mha_dropout_mask(Tq, Tk, B, heads, dropout, seed, q.device, diag) if dropout > 0 else None
+        for b in range(B):
+            dwb = dw[b].float() / heads                                   # (Tq, Tk), shared by the heads
+            for h0 in range(0, heads, hc):
+                h1 = min(heads, h0 + hc)
+                s = torch.matmul(qh[b, h0:h1], kh[b, h0:h1].transpose(-1, -2)) * scale
+                if causal is not None:
+                    s = s + causal
+                p = torch.exp(s - lse[b, h0:h1].unsqueeze(-1))           # the forward's softmax
+                del s
+                dp = dwb.expand(h1 - h0, Tq, Tk)
+                if dropout > 0:
+                    dp = dp * dmask[b, h0:h1]
+                ds = p * (dp - (dp * p).sum(-1, keepdim=True))
+                del p, dp
+                dq[b, h0:h1] = torch.matmul(ds, kh[b, h0:h1]) * scale
+                dk[b, h0:h1] = torch.matmul(ds.transpose(-1, -2), qh[b, h0:h1]) * scale
+        dq = dq.permute(2, 0, 1, 3).reshape(Tq, B, E)
+        dk = dk.permute(2, 0, 1, 3).reshape(Tk, B, E)
         return dq.to(q.dtype), dk.to(k.dtype), None, None, None, None, None, None
 
 

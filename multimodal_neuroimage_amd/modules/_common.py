@@ -4,7 +4,9 @@ The buffers built here (relative_position_index, attn_mask, relative_coords_tabl
 state_dicts keep the reference's keys and shapes; the HIP kernels compute the
 index and the mask analytically and never read them.
 """
+import collections
 import math
+import weakref
 
 import torch
 import torch.nn as nn
@@ -102,42 +104,56 @@ def _factorizations(n, k):
                 yield (a,) + rest
 
 
-_MASK_GEOMETRY = {}
+_MASK_GEOMETRY = collections.OrderedDict()   # (id, version, shape, window, device) -> (weakref, result)
+_MASK_GEOMETRY_MAX = 64
+
+
+def _mask_geometry_search(m, window):
+    nW, N, _ = m.shape
+    if N != math.prod(window):
+        return None
+    if not bool(m.any()):
+        # an all-zero mask is an unshifted layer (no pair masked): nW windows along the first
+        # non-trivial axis, shift 0
+        a = next((i for i, w in enumerate(window) if w > 1), 0)
+        return tuple(w * (nW if i == a else 1) for i, w in enumerate(window)), tuple(0 for _ in window)
+    for counts in _factorizations(nW, len(window)):
+        if any(c > 1 and w == 1 for c, w in zip(counts, window)):
+            continue
+        res = tuple(c * w for c, w in zip(counts, window))
+        for s in range(1, max(window)):
+            shift = tuple(s if w > s else 0 for w in window)
+            lab = shift_label_windows(res, window, shift, device=m.device)
+            ok = True
+            for w0 in range(0, nW, 256):
+                lb = lab[w0:w0 + 256]
+                cand = (lb.unsqueeze(1) != lb.unsqueeze(2)).to(m.dtype) * -100.0
+                if not torch.equal(cand, m[w0:w0 + 256]):
+                    ok = False
+                    break
+            if ok:
+                return res, shift
+    return None
 
 
 def geometry_for_mask(mask, window):
     """(resolution, shift) of a shifted-window layer whose calculate_mask equals `mask` (nW, N, N),
-    or None.  Validated once per mask tensor version (cached).  The attention of a window depends
-    only on its own tokens and mask[w mod nW], so any geometry reproducing the mask gives the
-    reference's result."""
+    or None.  An all-zero mask is shift 0.  The attention of a window depends only on its own tokens
+    and mask[w mod nW], so any geometry reproducing the mask gives the reference's result.
+
+    Cached per live mask tensor: the key holds the tensor's identity and in-place version, and the
+    entry a weak reference to it, so a freed mask whose address (or id) a new tensor reuses is never
+    taken for it; the cache keeps at most _MASK_GEOMETRY_MAX entries (least recently used out)."""
     window = tuple(int(w) for w in window)
-    key = (mask.data_ptr(), mask._version, tuple(mask.shape), window, str(mask.device))
-    if key in _MASK_GEOMETRY:
-        return _MASK_GEOMETRY[key]
-    nW, N, _ = mask.shape
-    found = None
-    m = mask.detach()
-    if N == math.prod(window):
-        for counts in _factorizations(nW, len(window)):
-            if any(c > 1 and w == 1 for c, w in zip(counts, window)):
-                continue
-            res = tuple(c * w for c, w in zip(counts, window))
-            for s in range(1, max(window)):
-                shift = tuple(s if w > s else 0 for w in window)
-                lab = shift_label_windows(res, window, shift, device=m.device)
-                ok = True
-                for w0 in range(0, nW, 256):
-                    lb = lab[w0:w0 + 256]
-                    cand = (lb.unsqueeze(1) != lb.unsqueeze(2)).to(m.dtype) * -100.0
-                    if not torch.equal(cand, m[w0:w0 + 256]):
-                        ok = False
-                        break
-                if ok:
-                    found = (res, shift)
-                    break
-            if found:
-                break
-    _MASK_GEOMETRY[key] = found
+    key = (id(mask), mask._version, tuple(mask.shape), window, str(mask.device))
+    hit = _MASK_GEOMETRY.get(key)
+    if hit is not None and hit[0]() is mask:
+        _MASK_GEOMETRY.move_to_end(key)
+        return hit[1]
+    found = _mask_geometry_search(mask.detach(), window)
+    _MASK_GEOMETRY[key] = (weakref.ref(mask), found)
+    while len(_MASK_GEOMETRY) > _MASK_GEOMETRY_MAX:
+        _MASK_GEOMETRY.popitem(last=False)
     return found
 
 

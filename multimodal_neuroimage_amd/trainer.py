@@ -20,6 +20,7 @@ target); the ABCD file readers are out of scope, so callers (and th
 in the way the reference's own dataset registry does.
 """
 import csv
+import contextlib
 import os
 import warnings
 from itertools import zip_longest
@@ -34,6 +35,16 @@ from . import model as M
 from .learning_rate import LrHandler
 from .metrics import classification_metrics, regression_metrics
 
+
+@contextlib.contextmanager
+def roctx_range(name):
+    """A roctx range (torch.cuda.nvtx maps to roctx on ROCm) around a step phase, as the reference's
+    torch.cuda.nvtx.range_push/pop pairs (trainer.py:373-430); a no-op cost when no profiler listens."""
+    torch.cuda.nvtx.range_push(name)
+    try:
+        yield
+    finally:
+        torch.cuda.nvtx.range_pop()
 
 def reproducibility(**kwargs):
     """utils.py:134-142: seed torch (and its GPU generators) and numpy."""
@@ -396,13 +407,21 @@ class Trainer:
         acc = int(self.kwargs.get("accumulation_steps") or 1)
         for batch_idx, input_dict in enumerate(self.train_loader):
             self.writer.total_train_steps += 1
-            self.optimizer.zero_grad()
-            loss_dict, loss = self.forward_pass(input_dict)
-            (loss / acc).backward()
-            if (batch_idx + 1) % acc == 0:
-                if self.kwargs.get("gradient_clipping"):
-                    torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.kwargs.get("clip_max_norm"))
-                self.optimizer.step()
+            # roctx ranges at the reference's NVTX points (trainer.py:373-430): rocprofv3
+            # --marker-trace lines its kernel trace up with them
+            with roctx_range("training step"):
+                self.optimizer.zero_grad()
+                with roctx_range("forward"):
+                    loss_dict, loss = self.forward_pass(input_dict)
+                with roctx_range("backward"):
+                    (loss / acc).backward()
+                if (batch_idx + 1) % acc == 0:
+                    if self.kwargs.get("gradient_clipping"):
+                        with roctx_range("clip"):
+                            torch.nn.utils.clip_grad_norm_(self.model.parameters(),
+                                                           max_norm=self.kwargs.get("clip_max_norm"))
+                    with roctx_range("optimize"):
+                        self.optimizer.step()
             self.lr_handler.schedule_check_and_update(self.optimizer)
             self.writer.write_losses(loss_dict, set="train")
             if self.kwargs.get("profiling") and batch_idx == 10:

@@ -78,3 +78,27 @@ def test_mask_geometry_recovered_from_calculate_mask(res, window, shift):
     assert got is not None
     assert torch.equal(shift_mask_buffer(got[0], window, got[1]), mask)
     assert geometry_for_mask(torch.randn(mask.shape), window) is None
+
+
+def test_mask_geometry_cache_is_keyed_on_the_live_tensor():
+    """a cached geometry must never be returned for a different mask that reuses a freed
+    mask's identity, nor for a mask mutated in place; the cache stays bounded; an all-zero mask (an
+    unshifted layer) maps to shift 0."""
+    from multimodal_neuroimage_amd.modules import _common as Cm
+    window = (6, 6)
+    a = Cm.shift_mask_buffer((12, 12), window, (3, 3))
+    b = Cm.shift_mask_buffer((12, 12), window, (2, 2))
+    assert Cm.geometry_for_mask(a, window)[1] == (3, 3)
+    # same tensor object rewritten in place: a new version, recomputed
+    a.copy_(b)
+    assert Cm.geometry_for_mask(a, window)[1] == (2, 2)
+    # a stale entry (its tensor freed) is never served to another tensor, even one with the same key
+    key = next(reversed(Cm._MASK_GEOMETRY))
+    Cm._MASK_GEOMETRY[key] = (lambda: None, ((99, 99), (5, 5)))
+    assert Cm.geometry_for_mask(a, window)[1] == (2, 2)
+    for _ in range(3 * Cm._MASK_GEOMETRY_MAX):
+        Cm.geometry_for_mask(Cm.shift_mask_buffer((12, 12), window, (3, 3)), window)
+    assert len(Cm._MASK_GEOMETRY) <= Cm._MASK_GEOMETRY_MAX
+    z = torch.zeros(4, 36, 36)
+    res, shift = Cm.geometry_for_mask(z, window)
+    assert shift == (0, 0) and torch.equal(Cm.shift_mask_buffer(res, window, shift), z)
