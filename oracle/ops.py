@@ -144,10 +144,25 @@ def sinusoidal_positions(tokens):
     return torch.where(tokens != 0, pos, torch.zeros_like(pos))
 
 
+# Slope-pattern matching (tests only).  A LeakyReLU pre-activation within rounding of zero takes
+# one slope in an fp32 forward and possibly the other in the float64 oracle; its gradient then
+# differs by (1 - slope) over the receptive field of everything after it.  A test that wants to
+# compare gradients pointwise records which slope the fp32 kernel took at every LeakyReLU (the
+# sign of its output) and queues the masks here, in call order: each conv3d_cl with slope != 1
+# pops one and applies exactly that slope pattern instead of re-deciding from its own sign.
+SLOPE_PATTERNS = None
+
+
 def conv3d_cl(x, weight, bias=None, stride=1, pad=0, slope=1.0):
     """Channels-last Conv3d + LeakyReLU(slope): the 3D semantics of nn.Conv3d
     (nvidia_blocks.py:43) / the k=s patch-embed conv (swin_v2_module.py:483)."""
     y = F.conv3d(x.permute(0, 4, 1, 2, 3), weight, bias, stride=stride, padding=pad)
+    y = y.permute(0, 2, 3, 4, 1)
     if slope != 1.0:
-        y = F.leaky_relu(y, negative_slope=slope)
-    return y.permute(0, 2, 3, 4, 1).contiguous()
+        if SLOPE_PATTERNS:
+            pos = SLOPE_PATTERNS.pop(0).to(y.device)
+            assert pos.shape == y.shape, (pos.shape, y.shape)
+            y = torch.where(pos, y, y * slope)
+        else:
+            y = F.leaky_relu(y, negative_slope=slope)
+    return y.contiguous()

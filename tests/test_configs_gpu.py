@@ -1,0 +1,274 @@
+"""BASELINE configs exercised at their own workloads.
+
+* C5: the bf16 crossmodal MHA at the C5 sequence length T = 4,096 (12 heads, E = 84
+  and 168, causal) against the float64 oracle; one full C5 training step of SwinCrossmodal3D at its
+  own size (128^3 fMRI / patch 8 + 96^3 sMRI / patch 6, window 4, 4,096-token sequences, 12 layers,
+  8 pairs) with property checks; and a B = 1, 2-layer slice of the same model at the full volume
+  sizes against the float64 oracle composition.
+* C1: the build's Trainer running the 3D SwinFusion lift on synthetic 32^3 pairs
+  (window 4, patch 4, batch 2) for one epoch: first-step logits against the float64 oracle, finite
+  losses, checkpoint written in the reference schema and resumed.
+* The 2^23-row routing boundary of the merged window-attention backward (wattn.hip: rows >= 2^23
+  or row * stride >= 2^31 go to the generic kernel): a 10 x 96^3 batch (8,847,360 rows) through
+  the generic kernel against the merged kernel on its two halves (windows are independent).
+
+Tolerances: bf16 (C5) 2e-2 max-rel; fp32 model logits 1e-3 (north star); two fp32
+backward kernels against each other 1e-4 max-rel (each is held to 1e-4 of the fp64 oracle).
+"""
+import json
+import os
+import sys
+import tempfile
+
+import pytest
+import scipy.stats
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+import recipe  # noqa: E402
+
+from multimodal_neuroimage_amd import distributed as D  # noqa: E402
+from multimodal_neuroimage_amd import functional as MF  # noqa: E402
+from multimodal_neuroimage_amd import model as M  # noqa: E402
+from multimodal_neuroimage_amd import trainer as T  # noqa: E402
+from oracle import model as OM  # noqa: E402
+from oracle import ops as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+TOL_BF16 = 2e-2
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "trainer.json")
+
+
+def rel_err(a, b):
+    a, b = a.detach().double(), b.detach().double().to(a.device)
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+# ------------------------------------------------------------------------------------------------
+# C5: bf16 MHA at T = 4,096
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,E", [(2, 84), (1, 168)])
+def test_mha_bf16_c5_t4096_vs_fp64_oracle(device, B, E):
+    """bf16 q/k/v/dout at the C5 sequence length, causal, 12 heads (head_dim 7 / 14): out, dq, dk,
+    dv and the head-averaged weights against the fp64 oracle on the same bf16-rounded inputs."""
+    Tn, heads = 4096, 12
+    g = torch.Generator(device=device).manual_seed(4096 + E)
+    q, k, v, gout = (torch.randn(Tn, B, E, device=device, generator=g).bfloat16().double() for _ in range(4))
+    diag = O.causal_diag(Tn, Tn)
+    leaves = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    ref, ref_w = O.mha_core(*leaves, heads, diag)
+    (ref * gout).sum().backward()
+    del ref_w
+    dev = [t.bfloat16().requires_grad_(True) for t in (q, k, v)]
+    out, lse = MF.mha_core(*dev, heads, diag)
+    out.backward(gout.bfloat16())
+    w = MF.mha_mean_probs(dev[0], dev[1], lse, heads, diag)
+    torch.cuda.synchronize()
+    errs = dict(out=rel_err(out, ref), dq=rel_err(dev[0].grad, leaves[0].grad),
+                dk=rel_err(dev[1].grad, leaves[1].grad), dv=rel_err(dev[2].grad, leaves[2].grad))
+    # the weights: compare batch by batch (the fp64 reference re-evaluated without autograd)
+    with torch.no_grad():
+        _, ref_w = O.mha_core(q, k, v, heads, diag)
+    errs["weights"] = rel_err(w, ref_w)
+    print(f"C5 bf16 MHA T=4096 B={B} E={E}: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()))
+    assert out.dtype == torch.bfloat16 and all(t.grad.dtype == torch.bfloat16 for t in dev)
+    assert max(errs.values()) < TOL_BF16, errs
+
+
+# ------------------------------------------------------------------------------------------------
+# C5: the composite at its own size
+# ------------------------------------------------------------------------------------------------
+def c5_kwargs(layers=12):
+    return dict(fine_tune_task="binary_classification", volume_size=128, patch_size=8, volume_size_B=96,
+                patch_size_B=6, swin_embed_dim=12, window_size=4, swin_heads=3, cross_heads=6, swin_depth=2,
+                mlp_ratio=4.0, intermediate_vec=84, num_heads_mult=12, nlevels=layers, attn_dropout=0.0,
+                attn_dropout_u=0.0, relu_dropout=0.0, res_dropout=0.0, embed_dropout=0.0, out_dropout=0.0,
+                attn_mask=True, mixing="U2L_and_L2U", concat_method="concat", fmri_type="divided_frequency",
+                head_dtype="bf16")
+
+
+def test_c5_full_step_at_size(device):
+    """One C5 training step at the bench workload: 8 pairs of 128^3 fMRI + 96^3 sMRI, 16^3 tokens
+    per modality (4,096-token crossmodal sequences), 12 layers x 12 heads, bf16 head.  Loss and
+    every gradient finite, gradients in the parameters' fp32, the forward bitwise repeatable, and
+    the crossmodal head's bf16 MHA kernels actually at T = 4,096."""
+    torch.manual_seed(5)
+    m = M.SwinCrossmodal3D(**c5_kwargs()).to(device)
+    gen = torch.Generator(device=device).manual_seed(55555555)
+    A = torch.randn(8, 128, 128, 128, device=device, generator=gen)
+    Bv = torch.randn(8, 96, 96, 96, device=device, generator=gen)
+    y = torch.bernoulli(torch.full((8, 1), 0.5, device=device), generator=gen)
+    MF.KernelTimer.reset()
+    MF.KernelTimer.enabled = True
+    try:
+        out = m(A, Bv)["binary_classification"]
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(out, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        kern = MF.KernelTimer.summary()
+    finally:
+        MF.KernelTimer.enabled = False
+    assert out.shape == (8, 1) and out.dtype == torch.float32
+    assert torch.isfinite(loss).item()
+    n = 0
+    for k, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        n += 1
+        assert p.grad.dtype == torch.float32, k
+        assert torch.isfinite(p.grad).all().item(), k
+    assert n > 100
+    assert "mha_fwd_E84_bf16" in kern and "mha_bwd_E168_bf16" in kern, sorted(kern)
+    # the head's MHA ran at the C5 shape: 4 * T^2 * B * E FLOPs per forward launch
+    assert kern["mha_fwd_E84_bf16"]["flops_per_launch"] == 4.0 * 4096 * 4096 * 8 * 84
+    with torch.no_grad():
+        o1 = m(A, Bv)["binary_classification"]
+        o2 = m(A, Bv)["binary_classification"]
+    assert torch.equal(o1, o2)
+    assert rel_err(o1, out) < 1e-6   # the grad-enabled forward ran the same kernels
+
+
+def test_c5_full_volumes_two_layer_slice_vs_fp64_oracle(device):
+    """The C5 composite at its full volume sizes (128^3 / 96^3, window 4, 4,096-token sequences)
+    cut to one pair and 2 crossmodal layers: logits and input gradients against the float64 oracle
+    composition at the C5 tolerance (bf16 head)."""
+    m = M.SwinCrossmodal3D(**c5_kwargs(layers=2))
+    recipe.fill_params(m)
+    A = torch.from_numpy(recipe.randn(5200, (1, 128, 128, 128)))
+    Bv = torch.from_numpy(recipe.randn(5201, (1, 96, 96, 96)))
+    tgt = torch.tensor([[1.0]], device=device)
+    p = OM.params_of(m, torch.float64, device)
+    A64, B64 = A.to(device).double().requires_grad_(True), Bv.to(device).double().requires_grad_(True)
+    cfg = dict(patch=8, patch_B=6, window_size=4, swin_heads=3, cross_heads=6, depth=2, layers=2, heads=12)
+    OM.ATTN_CHUNK = 512
+    try:
+        ref = OM.swin_crossmodal_logits(p, A64, B64, cfg)
+        torch.nn.functional.binary_cross_entropy_with_logits(ref, tgt.double()).backward()
+    finally:
+        OM.ATTN_CHUNK = None
+    m = m.to(device)
+    Ad, Bd = A.to(device).requires_grad_(True), Bv.to(device).requires_grad_(True)
+    out = m(Ad, Bd)["binary_classification"]
+    torch.nn.functional.binary_cross_entropy_with_logits(out, tgt).backward()
+    torch.cuda.synchronize()
+    errs = dict(logits=rel_err(out, ref), dA=rel_err(Ad.grad, A64.grad), dB=rel_err(Bd.grad, B64.grad))
+    print("C5 full-volume slice: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()))
+    assert max(errs.values()) < TOL_BF16, errs
+
+
+# ------------------------------------------------------------------------------------------------
+# C1: the 3D lift through the Trainer
+# ------------------------------------------------------------------------------------------------
+class Synthetic3D(torch.utils.data.Dataset):
+    """Synthetic z-scored 32^3 sMRI / second-modality pairs in the reference dataset protocol
+    (index_l, dict items with the model inputs, 'subject', the target)."""
+
+    def __init__(self, **kwargs):
+        self.target = kwargs.get("target")
+        self.n = kwargs["n_subjects"]
+        self.side = kwargs["volume_size"]
+        self.index_l = [(i, f"SUBJ{i:03d}", None, None, torch.tensor(float(i % 3 == 0))) for i in range(self.n)]
+        self.augment = None
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        def vol(k):
+            v = recipe.randn(3000 * k + i, (self.side,) * 3)
+            return torch.Tensor(scipy.stats.zscore(v, axis=None))
+        return {"smri": vol(1), "dti": vol(2), "subject": i, "subject_name": f"SUBJ{i:03d}",
+                self.target: self.index_l[i][4]}
+
+
+def test_c1_trainer_3d_lift_32(device):
+    """SURVEY §8d C1 lift: SwinFusion 3D on 32^3 pairs, window 4 (window 1 would NaN the Swin-V2
+    cpb table, swin_v2_module.py:105-106), patch 4 (32 -> 8^3 -> 4^3 -> 2^3 head stages), batch 2,
+    one epoch through the build's Trainer with the reference's kwargs.  The first training step's
+    logits match the float64 oracle (1e-3), every loss is finite, the rank-0 checkpoint carries the
+    reference schema and a new Trainer resumes from it."""
+    g = json.load(open(GOLD))
+    kw = dict(g["kwargs"])
+    tmp = tempfile.mkdtemp()
+    kw.update(cuda=True, workers=0, experiment_folder=tmp, experiment_title="c1lift", n_subjects=16,
+              env=D.DistEnv(device=torch.device(device)), loaded_model_weights_path=None, volume_size=32,
+              window_size=4, patch_size=4, nEpochs=1, batch_size=2, samplers=None)
+    T.DataHandler.datasets["struct"] = Synthetic3D
+    tr = T.Trainer(sets=["train", "val"], **kw)
+    net = tr._net()
+    recipe.fill_params(net)
+    for mod in net.modules():   # the Swin-V2 head's hard-coded drop_path 0.1 is RNG: off
+        if hasattr(mod, "drop_prob"):
+            mod.drop_prob = 0.0
+    first = {}
+
+    def hook(mod, args, out):
+        if tr.mode == "train" and not first:
+            first["inputs"] = [a.detach().clone() for a in args]
+            first["logits"] = out["binary_classification"].detach().clone()
+            first["params"] = {k: v.detach().clone() for k, v in mod.named_parameters()}
+    h = net.register_forward_hook(hook)
+    tr.training()
+    h.remove()
+    losses = torch.stack([v.float() for v in tr.writer.values[("total", "train")]])
+    assert losses.numel() == len(tr.train_loader) >= 4
+    assert torch.isfinite(losses).all().item()
+    assert first["inputs"][0].shape == (2, 32, 32, 32)
+    # first-step logits against the float64 oracle with the step's own parameters
+    p = {k: v.double().requires_grad_(False) for k, v in first["params"].items()}
+    cfg = dict(window_size=4, Ex_depths=[6, 6], Fusion_depths=[2, 2, 2], Re_depths=[6, 6], heads=6,
+               resolution=(8, 8, 8), head_patch=4)
+    with torch.no_grad():
+        ref = OM.swinfusion_logits(p, first["inputs"][0].double(), first["inputs"][1].double(), cfg)
+    err = rel_err(first["logits"], ref)
+    print(f"C1 lift: first-step logits max-rel {err:.2e}, losses {[round(float(x), 4) for x in losses]}")
+    assert err < 1e-3, (first["logits"], ref)
+    # checkpoint (reference schema) and resume
+    pths = [f for f in os.listdir(tmp) if f.endswith(".pth")]
+    assert pths, "no checkpoint written"
+    ck = torch.load(os.path.join(tmp, sorted(pths, key=lambda f: os.path.getctime(os.path.join(tmp, f)))[-1]),
+                    map_location="cpu", weights_only=True)
+    for key in ("model_state_dict", "optimizer_state_dict", "epoch", "loss_value", "amp_state", "val_AUROC",
+                "val_threshold", "schedule_state_dict", "lr"):
+        assert key in ck, key
+    assert set(ck["model_state_dict"]) == set(net.state_dict())
+    tr2 = T.Trainer(sets=["train", "val"], **kw)
+    assert tr2.st_epoch == int(ck["epoch"]) + 1
+    for k, v in tr2._net().state_dict().items():
+        assert torch.equal(v.cpu(), ck["model_state_dict"][k].cpu()), k
+
+
+# ------------------------------------------------------------------------------------------------
+# the 2^23-row routing boundary of the merged backward
+# ------------------------------------------------------------------------------------------------
+def test_wattn_bwd_past_the_24bit_row_bound_matches_the_merged_kernel_on_halves(device):
+    """B = 10 at 96^3 (8,847,360 rows > 2^23): the host routes the backward to the generic kernel
+    (the merged one addresses dk / dv rows with 24-bit products).  Windows are independent and the
+    shift mask repeats per sample, so the two B = 5 halves (4,423,680 rows each, merged kernel) must
+    give the same dq / dk / dv rows and, summed, the same bias-table gradient."""
+    B, S, C, heads = 10, 96, 12, 6
+    window, shift = (6, 6, 6), (3, 3, 3)
+    full = MF.WindowGeometry(B, (S, S, S), window, shift)
+    half = MF.WindowGeometry(B // 2, (S, S, S), window, shift)
+    assert full.tokens > 1 << 23 > half.tokens
+    g = torch.Generator(device=device).manual_seed(23)
+    qkv = torch.randn(full.tokens, 3 * C, device=device, generator=g)
+    gout = torch.randn(full.tokens, C, device=device, generator=g)
+    table = torch.randn(full.table_rows, heads, device=device, generator=g) * 0.5
+    res = []
+    for geom, sl in ((full, slice(0, full.tokens)), (half, slice(0, half.tokens)),
+                     (half, slice(half.tokens, full.tokens))):
+        x = qkv[sl].clone().requires_grad_(True)
+        tab = table.clone().requires_grad_(True)
+        out = MF.window_attention_self(x, tab, geom, heads)
+        (out * gout[sl]).sum().backward()
+        res.append((out.detach(), x.grad, tab.grad))
+        del x, out
+    torch.cuda.synchronize()
+    (o, dx, dt), (o1, dx1, dt1), (o2, dx2, dt2) = res
+    assert torch.equal(o, torch.cat([o1, o2]))   # the forward has no such routing: same kernel, same rows
+    errs = dict(dq=rel_err(dx[:, :C], torch.cat([dx1, dx2])[:, :C]),
+                dk=rel_err(dx[:, C:2 * C], torch.cat([dx1, dx2])[:, C:2 * C]),
+                dv=rel_err(dx[:, 2 * C:], torch.cat([dx1, dx2])[:, 2 * C:]), dtable=rel_err(dt, dt1 + dt2))
+    print("2^23 boundary: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()))
+    assert max(errs.values()) < 1e-4, errs

@@ -10,8 +10,10 @@
 * C2: the single-modality 3D Swin-V2 (patch 8, depths [2, 2, 6], heads [3, 6, 12], 96^3 volumes,
   B = 4, stage resolutions 12 -> 6 -> 3) against the same oracle.
 
-Tolerances: 1e-4 max-rel for single kernels (as test_kernels_gpu.py), 1e-3 for model logits and
-input gradients (north-star bar), 2e-3 for parameter gradients (as test_composite_gpu.py)."""
+Tolerances: 1e-4 max-rel for single kernels (as test_kernels_gpu.py), 1e-3 max-rel for model
+logits and input gradients (north-star bar; SwinFusion's input gradients against the oracle driven
+with the GPU forward's LeakyReLU slope pattern, see _model_parity), 2e-3 for parameter gradients
+(as test_composite_gpu.py)."""
 import pytest
 import torch
 
@@ -75,43 +77,64 @@ def _no_drop_path(m):
             mod.drop_prob = 0.0
 
 
-def _input_grad_err(a, r):
-    """(max-norm rel error, L2 rel error, fraction of voxels off by > 1e-4 of the max) of an input
-    gradient.  The conv stacks next to the input end in LeakyReLU: a pre-activation within ~1e-7 of
-    zero takes the other slope in fp32 than in fp64, and the flipped voxel's gradient differs by
-    0.8x over the few-voxel receptive field of the convs after it.  Which voxels flip depends on
-    fp32 rounding order, so the max-norm error of the input gradient alone is a lottery (1e-5 or
-    1e-3 for the same model; scripts/diag_model_kinks.py: 182 of 221184 voxels in one 7^3 box).
-    The test bounds the L2 error, the max error loosely, and requires the outliers to be local."""
+def _l2_rel(a, r):
     a, r = a.detach().double(), r.detach().double().to(a.device)
-    d = (a - r).abs()
-    mx = r.abs().max().clamp_min(1e-12)
-    return (float(d.max() / mx), float(d.norm() / r.norm().clamp_min(1e-12)),
-            float((d > 1e-4 * mx).double().mean()))
+    return float((a - r).norm() / r.norm().clamp_min(1e-12))
 
 
-def _model_parity(device, m, ref_fn, inputs, tgt, ptol=2e-3):
-    recipe.fill_params(m)
-    _no_drop_path(m)
-    p = OM.params_of(m, torch.float64, device)
+def _oracle_run(device, p, ref_fn, inputs, tgt, patterns):
+    """float64 oracle logits + input gradients; `patterns`: the GPU forward's LeakyReLU slope
+    patterns (oracle/ops.py SLOPE_PATTERNS), or None for the oracle's own sign decisions."""
     ins64 = [t.to(device).double().requires_grad_(True) for t in inputs]
     OM.ATTN_CHUNK = 256
+    O.SLOPE_PATTERNS = list(patterns) if patterns is not None else None
     try:
         ref = ref_fn(p, *ins64)
         torch.nn.functional.binary_cross_entropy_with_logits(ref, tgt.to(device).double()).backward()
+        assert not O.SLOPE_PATTERNS, "slope patterns left over: the oracle and the model disagree on the LeakyReLUs"
     finally:
         OM.ATTN_CHUNK = None
+        O.SLOPE_PATTERNS = None
+    return ref, ins64
+
+
+def _model_parity(device, m, ref_fn, inputs, tgt, monkeypatch, ptol=2e-3):
+    """GPU model vs the float64 oracle: logits and input gradients at 1e-3 max-rel, every parameter
+    gradient at ptol.
+
+    The SwinFusion conv stacks end in LeakyReLU(0.2).  A pre-activation within rounding of zero
+    can take the other slope in fp32 than in fp64, and that voxel's gradient then differs by 0.8x
+    over the receptive field of the convs after it (r2i: 1.2e-3 max-rel on the input gradient of
+    sample 0, in one box of voxels).  So the pointwise checks run against the oracle driven with the
+    GPU forward's own slope pattern at every LeakyReLU (recorded from the sign of each fused
+    conv + LeakyReLU output): a voxel that still disagrees is a kernel error, not a kink.  The
+    un-matched oracle is checked too, on logits (1e-3) and the L2 error of the input gradients
+    (1e-3), which a few flipped kinks cannot move."""
+    from multimodal_neuroimage_amd.modules import swinfusion_module as SFM
+    recipe.fill_params(m)
+    _no_drop_path(m)
+    p = OM.params_of(m, torch.float64, device)
+    patterns = []
+    conv = SFM.conv3d_cl
+
+    def recording_conv(x, w, b, stride, pad, slope=1.0):
+        y = conv(x, w, b, stride, pad, slope)
+        if slope != 1.0:
+            patterns.append((y > 0).detach())
+        return y
+    monkeypatch.setattr(SFM, "conv3d_cl", recording_conv)
     m = m.to(device)
     ins = [t.to(device).requires_grad_(True) for t in inputs]
     out = m(*ins)["binary_classification"]
     torch.nn.functional.binary_cross_entropy_with_logits(out, tgt.to(device)).backward()
     torch.cuda.synchronize()
-    gerr = [_input_grad_err(a.grad, r.grad) for a, r in zip(ins, ins64)]
-    print(f"model parity: logits {rel_err(out, ref):.3e}, input grads (max, L2, voxel fraction > 1e-4 max) "
-          f"{'; '.join(', '.join(f'{v:.3e}' for v in e) for e in gerr)}")
+    monkeypatch.setattr(SFM, "conv3d_cl", conv)
+    ref, ins64 = _oracle_run(device, p, ref_fn, inputs, tgt, patterns)
+    errs = [rel_err(a.grad, r.grad) for a, r in zip(ins, ins64)]
+    print(f"model parity (slope-matched oracle, {len(patterns)} LeakyReLUs): logits {rel_err(out, ref):.3e}, "
+          f"input grads max-rel {', '.join(f'{e:.3e}' for e in errs)}")
     assert rel_err(out, ref) < 1e-3, (out, ref)
-    for e_max, e_l2, frac in gerr:
-        assert e_l2 < 1e-3 and e_max < 1e-2 and frac < 0.01, (e_max, e_l2, frac)
+    assert max(errs) < 1e-3, errs
     worst = {}
     for k, prm in m.named_parameters():
         r = p[k].grad
@@ -121,10 +144,19 @@ def _model_parity(device, m, ref_fn, inputs, tgt, ptol=2e-3):
         worst[k] = rel_err(prm.grad, r)
     bad = {k: e for k, e in worst.items() if e >= ptol}
     assert not bad, bad
+    if patterns:   # the un-matched oracle: logits and the L2 error of the input gradients
+        p2 = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+        ref2, ins64b = _oracle_run(device, p2, ref_fn, inputs, tgt, None)
+        l2 = [_l2_rel(a.grad, r.grad) for a, r in zip(ins, ins64b)]
+        print(f"model parity (un-matched oracle): logits {rel_err(out, ref2):.3e}, input grads L2 "
+              f"{', '.join(f'{e:.3e}' for e in l2)}, max-rel "
+              f"{', '.join(f'{rel_err(a.grad, r.grad):.3e}' for a, r in zip(ins, ins64b))}")
+        assert rel_err(out, ref2) < 1e-3
+        assert max(l2) < 1e-3, l2
     return worst
 
 
-def test_swinfusion3d_full_depth_48_vs_fp64_oracle(device):
+def test_swinfusion3d_full_depth_48_vs_fp64_oracle(device, monkeypatch):
     """The C3 topology (60 window-attention blocks, conv stacks, Swin-V2 head) at 48^3, B = 2."""
     kw = dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
               attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=48, patch_size=4,
@@ -135,11 +167,11 @@ def test_swinfusion3d_full_depth_48_vs_fp64_oracle(device):
     cfg = dict(window_size=6, Ex_depths=[6, 6], Fusion_depths=[2, 2, 2], Re_depths=[6, 6], heads=6,
                resolution=(12, 12, 12), head_patch=4)
     worst = _model_parity(device, m, lambda p, a, b: OM.swinfusion_logits(p, a, b, cfg), [A, Bv],
-                          torch.tensor([[1.0], [0.0]]))
+                          torch.tensor([[1.0], [0.0]]), monkeypatch)
     assert len(worst) > 300   # every trained tensor was compared
 
 
-def test_swin_v2_c2_96_b4_vs_fp64_oracle(device):
+def test_swin_v2_c2_96_b4_vs_fp64_oracle(device, monkeypatch):
     """C2: single-modality 3D Swin-V2, 96^3 volumes, B = 4 (stage resolutions 12 -> 6 -> 3)."""
     kw = dict(fine_tune_task="binary_classification", size_of_model="large", swin_embed_dim=12, drop_rate=0.0,
               attn_drop_rate=0.0, mlp_ratio=4.0, drop_path_rate=0.0, intermediate_vec=96, patch_size=8,
@@ -147,7 +179,7 @@ def test_swin_v2_c2_96_b4_vs_fp64_oracle(device):
     m = M.SwinTransformerV2(**kw)
     x = torch.from_numpy(recipe.randn(8200, (4, 96, 96, 96)))
     worst = _model_parity(device, m, lambda p, a: OM.swin_v2_logits(p, "", a, 8, 6), [x],
-                          torch.tensor([[1.0], [0.0], [1.0], [1.0]]))
+                          torch.tensor([[1.0], [0.0], [1.0], [1.0]]), monkeypatch)
     assert any("layers.2.blocks.5" in k for k in worst)
 
 
@@ -180,8 +212,8 @@ def test_swinfusion3d_checkpointed_blocks_match_plain(device):
     for a, b in zip(g1, g2):
         assert torch.equal(a, b)
     assert p1.keys() == p2.keys()
-    for k in p1:
+    for k in p1:   # every weight gradient is a fixed-order reduction (dtau included since r3)
         if p1[k] is None:
             assert p2[k] is None, k
-        else:   # the Swin-V2 head's dtau (logit_scale) sums in a different order: not bitwise
-            assert rel_err(p1[k], p2[k]) < 1e-5, k
+        else:
+            assert torch.equal(p1[k], p2[k]), (k, rel_err(p1[k], p2[k]))

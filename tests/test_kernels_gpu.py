@@ -652,6 +652,31 @@ def test_window_attention_grads_are_deterministic(device, cross):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("C,heads,spatial,window", [(12, 3, (24, 24, 18), (6, 6, 6)), (12, 6, (16, 16, 16), (4, 4, 4)),
+                                                    (48, 12, (3, 3, 3), (3, 3, 3)), (24, 6, (12, 12, 12), (6, 6, 6))])
+def test_swin_v2_attention_grads_are_deterministic(device, C, heads, spatial, window):
+    """Kind 1 (Swin-V2 cosine attention): dq/dk/dv, the bias-table gradient (64-bit fixed point) and
+    dtau (logit_scale: per-block partial rows + a fixed-order column sum, no float atomics) are
+    bitwise identical across runs, on the packed (head_dim 2) and generic (head_dim 4) kernels."""
+    shift = tuple(w // 2 if s > w else 0 for s, w in zip(spatial, window))
+    geom = MF.WindowGeometry(2, spatial, window, shift)
+    torch.manual_seed(13 + C)
+    qkv0 = torch.randn(geom.tokens, 3 * C, device=device)
+    table = (torch.randn(geom.table_rows, heads, device=device) * 4).requires_grad_(True)
+    tau = (torch.rand(heads, device=device) * 15 + 5).requires_grad_(True)
+    g = torch.randn(geom.tokens, C, device=device)
+    res = []
+    for _ in range(3):
+        table.grad = tau.grad = None
+        qkv = qkv0.clone().requires_grad_(True)
+        out = MF.window_attention_self(qkv, table, geom, heads, kind=1, tau=tau)
+        (out * g).sum().backward()
+        res.append((qkv.grad, table.grad.clone(), tau.grad.clone()))
+    for r in res[1:]:
+        for a, b in zip(r, res[0]):
+            assert torch.equal(a, b)
+
+
 MHA_DROP = [
     # Tq, Tk, B, heads, hd, causal, p
     (64, 64, 2, 4, 7, True, 0.1),
