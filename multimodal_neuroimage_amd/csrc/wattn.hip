@@ -788,11 +788,7 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
                        row_aligned(dout, d->o_stride, d->C) && row_aligned(dq, d->q_stride, d->C) &&
                        row_aligned(dk, d->k_stride, d->C) && row_aligned(dv, d->v_stride, d->C),
                    "wattn_bwd: tensors must be 16-byte aligned with strides multiple of 4");
-    // the merged backward addresses dk / dv rows with 24-bit products (row < 2^23, row * stride < 2^31)
-    const int64_t bc_rows = (int64_t)a.g.B * a.g.D * a.g.H * a.g.W;
-    const int64_t bc_ld = d->k_stride > d->v_stride ? d->k_stride : d->v_stride;
-    if (wattn_bc_supported(a.g, d->C, d->heads, d->kind) && bc_rows < (1 << 23) && bc_ld < (1 << 23) &&
-        bc_rows * bc_ld < ((int64_t)1 << 31)) {
+    if (wattn_bc_supported(a.g, d->C, d->heads, d->kind)) {   // 64-bit row addressing: any token count
         a.q = q; a.k = k; a.v = v; a.table = table; a.tau = table; a.lse = const_cast<float*>(lse);
         a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtable;
         return wattn_bc_backward(a, d->heads, dtable, workspace, (hipStream_t)stream);

@@ -307,7 +307,6 @@ __device__ __forceinline__ Work work(int NHG, int wave) {
 // key) instead of once in each pass.  Deterministic (fixed lane tree, fixed row order).
 // ------------------------------------------------------------------------------------
 namespace q4 {
-__constant__ unsigned char kInvPermQ[NB] = {0, 1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 22, 23, 24, 25, 26, 27, 32, 33, 34, 28, 29, 30, 35, 36, 6, 7, 8, 9, 37, 38, 17, 18, 19, 20, 39, 40, 41, 21, 42, 43, 44, 45, 31, 46, 47, 48, 49, 50, 10, 51, 52, 53};
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {
@@ -324,7 +323,13 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
     b = __uint_as_float(r[1]);
 }
 
-// 16 f2 partials per lane -> lane l returns the 64-lane sum of value l >> 1
+// 16 f2 partials per lane -> lane l returns the 64-lane sum of value l >> 1.  Stages 1-2 swap
+// register halves across lane halves (v_permlane32_swap / v_permlane16_swap: one instruction per
+// register pair).  Stages 3-6 pair lanes l and l ^ d inside a row; there every lane forms BOTH
+// candidate sums with the DPP operand folded into v_add_f32 (x + dpp(x), one instruction each) and
+// keeps the one its lane bit selects -- 3 instructions per output float instead of two selects, a
+// zero-initialised v_mov_b32_dpp and half a packed add.  The operand order (own value first,
+// partner's second) is that of the keep/send formulation, so the sums are bitwise the same.
 __device__ __forceinline__ float reduce32(f2 (&P)[16], int lane) {
     f2 R[8];
 #pragma unroll
@@ -343,18 +348,22 @@ __device__ __forceinline__ float reduce32(f2 (&P)[16], int lane) {
         S[k] = (f2){a0, a1} + (f2){b0, b1};
     }
     const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
-    f2 T[2];
+    // lane bit 3: key 0 or 1 of the pair (row_ror:8 partner = lane ^ 8)
+    float T[4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {   // lane bit 3: key 0 or 1 of the pair (row_ror:8 partner = lane ^ 8)
-        const f2 keep = b3 ? S[k + 2] : S[k], send = b3 ? S[k] : S[k + 2];
-        T[k] = keep + (f2){dpp<0x128>(send.x), dpp<0x128>(send.y)};
+    for (int k = 0; k < 2; ++k) {
+        const float lo_x = S[k].x + dpp<0x128>(S[k].x), hi_x = S[k + 2].x + dpp<0x128>(S[k + 2].x);
+        const float lo_y = S[k].y + dpp<0x128>(S[k].y), hi_y = S[k + 2].y + dpp<0x128>(S[k + 2].y);
+        T[2 * k] = b3 ? hi_x : lo_x;
+        T[2 * k + 1] = b3 ? hi_y : lo_y;
     }
     // lane bit 2: dim c (row_half_mirror partner = lane ^ 7 within 8)
-    const f2 keep = b2 ? T[1] : T[0], send = b2 ? T[0] : T[1];
-    const f2 U = keep + (f2){dpp<0x141>(send.x), dpp<0x141>(send.y)};
+    const float u0 = T[0] + dpp<0x141>(T[0]), u2 = T[2] + dpp<0x141>(T[2]);
+    const float u1 = T[1] + dpp<0x141>(T[1]), u3 = T[3] + dpp<0x141>(T[3]);
+    const float Ux = b2 ? u2 : u0, Uy = b2 ? u3 : u1;
     // lane bit 1: head h (quad partner lane ^ 2), then lane ^ 1
-    const float kv = b1 ? U.y : U.x, sv = b1 ? U.x : U.y;
-    const float V = kv + dpp<0x4E>(sv);
+    const float vx = Ux + dpp<0x4E>(Ux), vy = Uy + dpp<0x4E>(Uy);
+    const float V = b1 ? vy : vx;
     return V + dpp<0xB1>(V);
 }
 }  // namespace q4
@@ -370,13 +379,14 @@ __device__ __forceinline__ f2 zero2() {
 template <bool MASKED, bool FOLD>
 __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
                                          const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
-                                         const bc::Regions& reg, char* sm, int kvw, int dtw, bool lane_ok,
-                                         const int (&rowk)[4], float* kout, int64_t kstride, float kscale) {
+                                         const bc::Regions& reg, char* sm, int kvw, int dtw, bool lane_ok) {
     using namespace q4;
     const int lane = threadIdx.x & 63;
-    const char* kv = sm + kvw;
+    char* kv = sm + kvw;
     const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
-    const int vsel = (lane >> 3) & 3;   // the key whose sum this lane ends with (l >> 1 = kind, v, c, h)
+    // where this lane's key-side sum (value l >> 1 = kind, key v, dim c, head h) goes: the step's
+    // key-quad record, dead once the step has read it, as [v][kind][h c] (the rows' natural order)
+    const int soff = ((lane >> 3) & 3) * 32 + (lane >> 5) * 16 + ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4;
     // The table image offset goes through an empty asm after each step's stores, so the compiler
     // treats the next step's table reads as possibly aliasing them (other lanes' entries) and keeps
     // them behind the stores; LDS executes a wave's accesses in order, so no wait is needed.  (Issuing
@@ -449,14 +459,9 @@ __device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], 
                 asm volatile("" : "+v"(dto));   // next reads: behind the stores above (see the top)
                 // all 64 lanes take part in the reduction (spare lanes contribute zeros)
                 const float sum = reduce32(P, lane);
-                // rows of key quad n = (zr, yr, x): held by the lane that owns query quad n
-                const int owner = kInvPermQ[(zr * 3 + yr) * 6 + x];
-                const int r0 = __builtin_amdgcn_readlane(rowk[0], owner), r1 = __builtin_amdgcn_readlane(rowk[1], owner);
-                const int r2 = __builtin_amdgcn_readlane(rowk[2], owner), r3 = __builtin_amdgcn_readlane(rowk[3], owner);
-                const int r = vsel == 0 ? r0 : (vsel == 1 ? r1 : (vsel == 2 ? r2 : r3));
-                // 24-bit multiply (full rate; the 64-bit product took two v_mul_lo_u32 and a
-                // v_mad_u64_u32): the host routes row counts / strides past 2^23 / 2^31 elsewhere
-                if ((lane & 1) == 0) kout[(uint32_t)__mul24(r, (int)kstride)] = sum * kscale;
+                // the final sums of key quad n = (zr, yr, x) replace its record (read above: LDS
+                // runs a wave's accesses in order); the owner lane writes the rows out after the walk
+                if ((lane & 1) == 0) *reinterpret_cast<float*>(kv + ((zr * 3 + yr) * 6 + x) * REC + soff) = sum;
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -485,18 +490,13 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
     const int kvw = wave * KVB, dtw = DT + wave * TABB;
     const int coff = wk.hp * 4;
     const f2 qscale = bc::splat(a.scale * kLog2e);
-    // this lane's output slot of the key-side sums: value l >> 1 = (kind, key, dim c, head h)
-    const bool is_dv = lane & 32;
-    const int comp = ((lane >> 1) & 1) * 2 + ((lane >> 2) & 1);   // global row order (h0c0, h0c1, h1c0, h1c1)
-    float* kout = (is_dv ? a.dv : a.dk) + coff + comp;
-    const int64_t kstride = is_dv ? a.vs : a.ks;
-    const float kscale = is_dv ? 1.0f : kLn2;   // dk: the staged q carries scale * log2 e
     for (int j = wk.j0;; j += wk.dj) {
         const int w = wk.xcd + 8 * j;
         if (w >= g.nwin) break;
         Row q[4], dO[4], dq[4];
         f2 lse2[4], ndl[4];
-        int rq[4] = {0, 0, 0, 0}, rowk[4] = {0, 0, 0, 0};
+        int rq[4] = {0, 0, 0, 0};
+        int64_t rowk[4] = {0, 0, 0, 0};
         const bc::Regions reg = bc::window_regions(g, w);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -507,7 +507,7 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
-                rowk[u] = (int)ti.row;
+                rowk[u] = ti.row;
                 rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
                 const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
                 const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
@@ -537,8 +537,7 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
                 ndl[u] *= e;
             }
         }
-#define MMNI_Q4M(M, F) \
-    q4M_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw, lane_ok, rowk, kout, kstride, kscale)
+#define MMNI_Q4M(M, F) q4M_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw, lane_ok)
         if (fold) {
             if (reg.masked) MMNI_Q4M(true, true);
             else MMNI_Q4M(false, true);
@@ -548,8 +547,17 @@ void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
         }
 #undef MMNI_Q4M
         if (lane_ok) {
+            // dq from registers; dk / dv of this lane's key quad from its record slot (the walk
+            // left the final sums there), one 16-byte piece per row and kind
+            const char* rec = sm + kvw + beta * REC;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) bc::store_row_nat(a.dq + (int64_t)rowk[u] * a.qs + coff, dq[u], a.scale);
+            for (int u = 0; u < 4; ++u) {
+                bc::store_row_nat(a.dq + rowk[u] * a.qs + coff, dq[u], a.scale);
+                const bc::f4 dkr = *reinterpret_cast<const bc::f4*>(rec + u * 32);
+                const bc::f4 dvr = *reinterpret_cast<const bc::f4*>(rec + u * 32 + 16);
+                *reinterpret_cast<bc::f4*>(a.dk + rowk[u] * a.ks + coff) = dkr * kLn2;   // q carried scale * log2 e
+                *reinterpret_cast<bc::f4*>(a.dv + rowk[u] * a.vs + coff) = dvr;
+            }
         }
         asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
     }

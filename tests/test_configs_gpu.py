@@ -8,9 +8,10 @@
 * C1: the build's Trainer running the 3D SwinFusion lift on synthetic 32^3 pairs
   (window 4, patch 4, batch 2) for one epoch: first-step logits against the float64 oracle, finite
   losses, checkpoint written in the reference schema and resumed.
-* The 2^23-row routing boundary of the merged window-attention backward (wattn.hip: rows >= 2^23
-  or row * stride >= 2^31 go to the generic kernel): a 10 x 96^3 batch (8,847,360 rows) through
-  the generic kernel against the merged kernel on its two halves (windows are independent).
+* Row addressing past 2^23 rows (round 2's merged window-attention backward addressed dk / dv rows
+  with 24-bit products and routed bigger batches to the generic kernel; since round 3 it writes them
+  from LDS with 64-bit row offsets and takes every batch): a 10 x 96^3 batch (8,847,360 rows)
+  against the same kernel on its two halves (windows are independent).
 
 Tolerances: bf16 (C5) 2e-2 max-rel; fp32 model logits 1e-3 (north star); two fp32
 backward kernels against each other 1e-4 max-rel (each is held to 1e-4 of the fp64 oracle).
@@ -152,7 +153,8 @@ def test_c5_full_volumes_two_layer_slice_vs_fp64_oracle(device):
     torch.nn.functional.binary_cross_entropy_with_logits(out, tgt).backward()
     torch.cuda.synchronize()
     errs = dict(logits=rel_err(out, ref), dA=rel_err(Ad.grad, A64.grad), dB=rel_err(Bd.grad, B64.grad))
-    print("C5 full-volume slice: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()))
+    print("C5 full-volume slice: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()),
+          f"logits {out.detach().double().cpu().reshape(-1).tolist()} ref {ref.detach().cpu().reshape(-1).tolist()}")
     assert max(errs.values()) < TOL_BF16, errs
 
 
@@ -241,11 +243,12 @@ def test_c1_trainer_3d_lift_32(device):
 # ------------------------------------------------------------------------------------------------
 # the 2^23-row routing boundary of the merged backward
 # ------------------------------------------------------------------------------------------------
-def test_wattn_bwd_past_the_24bit_row_bound_matches_the_merged_kernel_on_halves(device):
-    """B = 10 at 96^3 (8,847,360 rows > 2^23): the host routes the backward to the generic kernel
-    (the merged one addresses dk / dv rows with 24-bit products).  Windows are independent and the
-    shift mask repeats per sample, so the two B = 5 halves (4,423,680 rows each, merged kernel) must
-    give the same dq / dk / dv rows and, summed, the same bias-table gradient."""
+def test_wattn_bwd_past_2_23_rows_matches_its_two_halves(device):
+    """B = 10 at 96^3 (8,847,360 rows > 2^23; 24-bit row products would wrap).  Windows are
+    independent and the shift mask repeats per sample, so the two B = 5 halves (4,423,680 rows
+    each) must give bitwise the same out / dq / dk / dv rows (each window's arithmetic does not
+    depend on where it sits in the batch) and, summed, the same bias-table gradient (the blocks'
+    partial rows group the windows differently: 1e-5)."""
     B, S, C, heads = 10, 96, 12, 6
     window, shift = (6, 6, 6), (3, 3, 3)
     full = MF.WindowGeometry(B, (S, S, S), window, shift)
@@ -266,9 +269,8 @@ def test_wattn_bwd_past_the_24bit_row_bound_matches_the_merged_kernel_on_halves(
         del x, out
     torch.cuda.synchronize()
     (o, dx, dt), (o1, dx1, dt1), (o2, dx2, dt2) = res
-    assert torch.equal(o, torch.cat([o1, o2]))   # the forward has no such routing: same kernel, same rows
-    errs = dict(dq=rel_err(dx[:, :C], torch.cat([dx1, dx2])[:, :C]),
-                dk=rel_err(dx[:, C:2 * C], torch.cat([dx1, dx2])[:, C:2 * C]),
-                dv=rel_err(dx[:, 2 * C:], torch.cat([dx1, dx2])[:, 2 * C:]), dtable=rel_err(dt, dt1 + dt2))
-    print("2^23 boundary: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()))
-    assert max(errs.values()) < 1e-4, errs
+    assert torch.equal(o, torch.cat([o1, o2]))
+    assert torch.equal(dx, torch.cat([dx1, dx2]))
+    err = rel_err(dt, dt1 + dt2)
+    print(f"2^23 rows: dq/dk/dv bitwise, dtable {err:.2e}")
+    assert err < 1e-5, err
