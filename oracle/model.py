@@ -281,10 +281,11 @@ def crossmodal_head(p, pre, x_l, x_u, layers, heads, feature_map_gen="no", attn_
     return out_cls, _lin(p, pre + "out_layer2", out_cls)
 
 
-def swin_crossmodal_logits(p, A, Bv, cfg):
+def swin_crossmodal_logits(p, A, Bv, cfg, return_embedding=False):
     """SwinCrossmodal3D (SURVEY §8d C4 composite): per modality Conv3d(k=s=patch) + LN + Swin-V2
     stage 1, Cross_BasicLayer, Linear to d, crossmodal head.  cfg: patch, window_size, swin_heads,
-    cross_heads, depth, layers, heads [, patch_B: modality B's patch (C5), default patch]."""
+    cross_heads, depth, layers, heads [, patch_B: modality B's patch (C5), default patch].
+    return_embedding: also return the head's out_cls ('embedding_per_ROIs', model.py:512-537)."""
     ws = cfg["window_size"]
     patches = {"A": cfg["patch"], "B": cfg.get("patch_B", cfg["patch"])}
 
@@ -303,9 +304,9 @@ def swin_crossmodal_logits(p, A, Bv, cfg):
     x, res = stage(A, "A")
     y, _ = stage(Bv, "B")
     x, y = cross_layer(p, "cross", x, y, res, cfg["depth"], cfg["cross_heads"], ws, res)
-    _, logits = crossmodal_head(p, "crossmodal.", _lin(p, "to_seq_A", x), _lin(p, "to_seq_B", y), cfg["layers"],
-                                cfg["heads"])
-    return logits
+    out_cls, logits = crossmodal_head(p, "crossmodal.", _lin(p, "to_seq_A", x), _lin(p, "to_seq_B", y),
+                                      cfg["layers"], cfg["heads"])
+    return (logits, out_cls) if return_embedding else logits
 
 
 def params_of(module, dtype=torch.float64, device=None):

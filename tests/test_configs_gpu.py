@@ -13,8 +13,8 @@
   from LDS with 64-bit row offsets and takes every batch): a 10 x 96^3 batch (8,847,360 rows)
   against the same kernel on its two halves (windows are independent).
 
-Tolerances: bf16 (C5) 2e-2 max-rel; fp32 model logits 1e-3 (north star); two fp32
-backward kernels against each other 1e-4 max-rel (each is held to 1e-4 of the fp64 oracle).
+Tolerances: bf16 (C5) 2e-2 max-rel; fp32 model logits 1e-3 (north star); the
+2^23-row case bitwise (same kernel, independent windows) except the bias-table gradient (1e-5).
 """
 import json
 import os
@@ -131,28 +131,34 @@ def test_c5_full_step_at_size(device):
 
 def test_c5_full_volumes_two_layer_slice_vs_fp64_oracle(device):
     """The C5 composite at its full volume sizes (128^3 / 96^3, window 4, 4,096-token sequences)
-    cut to one pair and 2 crossmodal layers: logits and input gradients against the float64 oracle
-    composition at the C5 tolerance (bf16 head)."""
+    cut to two pairs and 2 crossmodal layers, against the float64 oracle composition at the C5
+    tolerance (bf16 head): the head's 84-wide embedding (out_cls) and the input gradients at 2e-2
+    max-rel; the logit = out_layer2(out_cls) is a single projection that can cancel to near zero, so
+    its error is held to 2e-2 of its Cauchy-Schwarz scale |w2| |out_cls| + |b2|."""
     m = M.SwinCrossmodal3D(**c5_kwargs(layers=2))
     recipe.fill_params(m)
-    A = torch.from_numpy(recipe.randn(5200, (1, 128, 128, 128)))
-    Bv = torch.from_numpy(recipe.randn(5201, (1, 96, 96, 96)))
-    tgt = torch.tensor([[1.0]], device=device)
+    A = torch.from_numpy(recipe.randn(5200, (2, 128, 128, 128)))
+    Bv = torch.from_numpy(recipe.randn(5201, (2, 96, 96, 96)))
+    tgt = torch.tensor([[1.0], [0.0]], device=device)
     p = OM.params_of(m, torch.float64, device)
     A64, B64 = A.to(device).double().requires_grad_(True), Bv.to(device).double().requires_grad_(True)
     cfg = dict(patch=8, patch_B=6, window_size=4, swin_heads=3, cross_heads=6, depth=2, layers=2, heads=12)
     OM.ATTN_CHUNK = 512
     try:
-        ref = OM.swin_crossmodal_logits(p, A64, B64, cfg)
+        ref, ref_emb = OM.swin_crossmodal_logits(p, A64, B64, cfg, return_embedding=True)
         torch.nn.functional.binary_cross_entropy_with_logits(ref, tgt.double()).backward()
     finally:
         OM.ATTN_CHUNK = None
     m = m.to(device)
     Ad, Bd = A.to(device).requires_grad_(True), Bv.to(device).requires_grad_(True)
-    out = m(Ad, Bd)["binary_classification"]
+    res = m(Ad, Bd)
+    out, emb = res["binary_classification"], res["embedding_per_ROIs"]
     torch.nn.functional.binary_cross_entropy_with_logits(out, tgt).backward()
     torch.cuda.synchronize()
-    errs = dict(logits=rel_err(out, ref), dA=rel_err(Ad.grad, A64.grad), dB=rel_err(Bd.grad, B64.grad))
+    w2, b2 = p["crossmodal.out_layer2.weight"].detach(), p["crossmodal.out_layer2.bias"].detach()
+    scale = (w2.norm() * ref_emb.detach().norm(dim=-1) + b2.abs()).reshape(-1, 1)
+    errs = dict(embedding=rel_err(emb, ref_emb), dA=rel_err(Ad.grad, A64.grad), dB=rel_err(Bd.grad, B64.grad),
+                logits_vs_scale=float(((out.double() - ref.detach()).abs() / scale).max()))
     print("C5 full-volume slice: " + ", ".join(f"{n} {e:.2e}" for n, e in errs.items()),
           f"logits {out.detach().double().cpu().reshape(-1).tolist()} ref {ref.detach().cpu().reshape(-1).tolist()}")
     assert max(errs.values()) < TOL_BF16, errs
@@ -169,7 +175,8 @@ class Synthetic3D(torch.utils.data.Dataset):
         self.target = kwargs.get("target")
         self.n = kwargs["n_subjects"]
         self.side = kwargs["volume_size"]
-        self.index_l = [(i, f"SUBJ{i:03d}", None, None, torch.tensor(float(i % 3 == 0))) for i in range(self.n)]
+        self.index_l = [(i, f"SUBJ{i:03d}", None, None, torch.tensor(float((i * 7 + 3) % 5 < 2)))
+                        for i in range(self.n)]
         self.augment = None
 
     def __len__(self):
@@ -192,7 +199,7 @@ def test_c1_trainer_3d_lift_32(device):
     g = json.load(open(GOLD))
     kw = dict(g["kwargs"])
     tmp = tempfile.mkdtemp()
-    kw.update(cuda=True, workers=0, experiment_folder=tmp, experiment_title="c1lift", n_subjects=16,
+    kw.update(cuda=True, workers=0, experiment_folder=tmp, experiment_title="c1lift", n_subjects=g["n_subjects"],
               env=D.DistEnv(device=torch.device(device)), loaded_model_weights_path=None, volume_size=32,
               window_size=4, patch_size=4, nEpochs=1, batch_size=2, samplers=None)
     T.DataHandler.datasets["struct"] = Synthetic3D
@@ -213,7 +220,7 @@ def test_c1_trainer_3d_lift_32(device):
     tr.training()
     h.remove()
     losses = torch.stack([v.float() for v in tr.writer.values[("total", "train")]])
-    assert losses.numel() == len(tr.train_loader) >= 4
+    assert losses.numel() == len(tr.train_loader) >= 10
     assert torch.isfinite(losses).all().item()
     assert first["inputs"][0].shape == (2, 32, 32, 32)
     # first-step logits against the float64 oracle with the step's own parameters
