@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 5
+#define MMNI_ABI_VERSION 6
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -327,6 +327,49 @@ int mmni_zscore(int64_t n_arrays, int64_t count, const float* x, float* y, int h
 int mmni_fir_highpass_taps(int ntaps, double cutoff_frac, double* taps);
 int mmni_fmri_band_split(const mmni_bandsplit_desc* d, const float* y, const int32_t* lens, const double* taps,
                          float* raw, float* low, float* ultralow, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Crossmodal-encoder dense layers (ABI v6).  Token rows are the
+ * time-major (T, B, E) activations seen as (T*B, E) rows of row stride ld*.
+ *
+ *   mmni_rowgemm     y[r][n] = epi( sum_k x'[r][k] * W(n, k) ),  W(n, k) = w[n*w_sn + k*w_sk]
+ *                    (w_sk = 1: an nn.Linear weight (N, K); w_sn = 1: the transpose, for the
+ *                    input gradient dX = dY W of a Linear (K_lin, N_lin) -> (N = K_lin, K = N_lin))
+ *                    x' = LayerNorm_K(x) with gamma/beta/eps when ln (row mean / rstd written to
+ *                    mean / rstd when those are non-null), else x.
+ *                    epi: + bias[n] (nullable), ReLU when relu, * (aux[r][n] > 0) when aux is
+ *                    non-null (the ReLU backward), + res[r][n] when res is non-null.
+ *                    Replaces in one launch: layer_norms[i](x) -> F.linear -> F.relu -> + residual
+ *                    (crossmodal_transformer.py:145-165), the in_proj slices and out_proj of
+ *                    MultiheadAttention.forward (multihead_attention.py:71-84,129).
+ *   mmni_rowgemm_dw  dw[n][k] = sum_r dy[r][n] * x'[r][k], db[n] = sum_r dy[r][n] (db nullable);
+ *                    x' = LayerNorm recomputed from the forward's mean / rstd when ln.  Row
+ *                    chunks reduced in a fixed order: deterministic.  dy rows of stride ldy.
+ *   mmni_row_layernorm_bwd  dx = LayerNorm backward of dxn (+ dres), dgamma, dbeta over
+ *                    rows of C <= 256 (fixed-order partial sums: deterministic).
+ * All fp32.  Workspaces: mmni_rowgemm_dw_workspace_bytes / mmni_row_layernorm_bwd_workspace_bytes.
+ * ------------------------------------------------------------------------------------ */
+typedef struct mmni_rowgemm_desc {
+    int64_t rows;
+    int32_t K, N;
+    int64_t ldx, ldy, ldres, ldaux;
+    int64_t w_sn, w_sk;
+    int32_t ln;        /* LayerNorm prologue over the K input columns */
+    float eps;
+    int32_t relu;      /* ReLU epilogue */
+} mmni_rowgemm_desc;
+int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const float* gamma, const float* beta, const float* w,
+                 const float* bias, const float* aux, const float* res, float* y, float* mean, float* rstd,
+                 void* stream);
+size_t mmni_rowgemm_dw_workspace_bytes(const mmni_rowgemm_desc* d);
+int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const float* gamma, const float* beta,
+                    const float* mean, const float* rstd, const float* dy, float* dw, float* db, void* workspace,
+                    void* stream);
+size_t mmni_row_layernorm_bwd_workspace_bytes(int64_t rows, int C);
+int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
+                           const float* gamma, const float* mean, const float* rstd, const float* dres,
+                           int64_t ldres, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace,
+                           void* stream);
 
 int mmni_version(void);
 const char* mmni_last_error(void);

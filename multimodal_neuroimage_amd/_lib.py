@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -63,9 +63,21 @@ class BandSplitDesc(ctypes.Structure):
     _fields_ = [("B", _c_i32), ("R", _c_i32), ("Lmax", _c_i32), ("seq", _c_i32), ("ntaps", _c_i32)]
 
 
+class RowGemmDesc(ctypes.Structure):
+    _fields_ = [("rows", _c_i64), ("K", _c_i32), ("N", _c_i32), ("ldx", _c_i64), ("ldy", _c_i64),
+                ("ldres", _c_i64), ("ldaux", _c_i64), ("w_sn", _c_i64), ("w_sk", _c_i64), ("ln", _c_i32),
+                ("eps", _c_f), ("relu", _c_i32)]
+
+
 # symbol -> (restype, argtypes); every symbol include/mmni.h declares
 SIGNATURES = {
     "mmni_version": (_c_int, []),
+    "mmni_rowgemm": (_c_int, [ctypes.POINTER(RowGemmDesc)] + [_vp] * 11),
+    "mmni_rowgemm_dw_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RowGemmDesc)]),
+    "mmni_rowgemm_dw": (_c_int, [ctypes.POINTER(RowGemmDesc)] + [_vp] * 10),
+    "mmni_row_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
+    "mmni_row_layernorm_bwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp,
+                                        _c_i64, _vp, _vp, _vp, _vp]),
     "mmni_last_error": (ctypes.c_char_p, []),
     "mmni_wattn_fwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 9),
     "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 16),

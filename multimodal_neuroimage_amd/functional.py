@@ -972,3 +972,260 @@ class SplitKLinear(torch.nn.Linear):
 
     def forward(self, x):
         return _SplitKLinear.apply(x, self.weight, self.bias)
+
+
+# ------------------------------------------------------------------------------------------
+# crossmodal encoder layer on the HIP row-GEMM kernels (encoder.hip, ABI v6)
+# ------------------------------------------------------------------------------------------
+def _rg_desc(rows, K, N, ldx, ldy, w_sn, w_sk, ln=False, eps=0.0, relu=False, ldres=0, ldaux=0):
+    d = _lib.RowGemmDesc()
+    d.rows, d.K, d.N = int(rows), int(K), int(N)
+    d.ldx, d.ldy, d.ldres, d.ldaux = int(ldx), int(ldy), int(ldres), int(ldaux)
+    d.w_sn, d.w_sk = int(w_sn), int(w_sk)
+    d.ln, d.eps, d.relu = int(bool(ln)), float(eps), int(bool(relu))
+    return d
+
+
+def _rows_view(t, C):
+    """(rows, C) view of a tensor whose last dim is C with unit column stride and a uniform row
+    stride (contiguous time-major (T, B, C) tensors and column slices of packed rows)."""
+    if t.dim() == 2:
+        assert t.stride(1) == 1
+        return t
+    t2 = t.reshape(-1, C)
+    assert t2.stride(1) == 1
+    return t2
+
+
+def rowgemm(x2, w, bias=None, *, ln=None, relu=False, aux=None, res=None, transpose_w=False, stats=False):
+    """y = epi(x' W^T) on token rows with the HIP row-GEMM (mmni_rowgemm).
+
+    x2 (rows, K) with unit column stride; w an nn.Linear weight (N, K), or with transpose_w a weight
+    (K_lin = N_out, N_lin = K) whose input gradient dY W this is.  ln = (gamma, beta, eps): LayerNorm
+    prologue over the K columns; stats=True also returns the row (mean, rstd).  Epilogue: + bias,
+    ReLU, * (aux > 0), + res (rows, N)."""
+    require_device(x2, w, what="rowgemm")
+    rows, K = x2.shape
+    if transpose_w:
+        Kw, N = w.shape
+        w_sn, w_sk = 1, w.stride(0)
+        assert w.stride(1) == 1 and Kw == K
+    else:
+        N, Kw = w.shape
+        w_sn, w_sk = w.stride(0), 1
+        assert w.stride(1) == 1 and Kw == K
+    y = torch.empty(rows, N, device=x2.device, dtype=torch.float32)
+    mean = rstd = None
+    gamma = beta = None
+    eps = 0.0
+    if ln is not None:
+        gamma, beta, eps = ln
+        if stats:
+            mean = torch.empty(rows, device=x2.device, dtype=torch.float32)
+            rstd = torch.empty(rows, device=x2.device, dtype=torch.float32)
+    d = _rg_desc(rows, K, N, x2.stride(0), N, w_sn, w_sk, ln is not None, eps, relu,
+                 res.stride(0) if res is not None else 0, aux.stride(0) if aux is not None else 0)
+    ev = KernelTimer.start()
+    check(_lib.load().mmni_rowgemm(ctypes.byref(d), ptr(x2), ptr(gamma), ptr(beta), ptr(w), ptr(bias), ptr(aux),
+                                   ptr(res), ptr(y), ptr(mean), ptr(rstd), stream_handle(x2.device)), "mmni_rowgemm")
+    KernelTimer.stop(f"rowgemm_{K}x{N}{'_ln' if ln is not None else ''}", ev, 2.0 * rows * K * N,
+                     4.0 * rows * (K + N + (N if res is not None else 0) + (N if aux is not None else 0)))
+    return (y, mean, rstd) if stats else y
+
+
+def rowgemm_dw(x2, dy2, N, K, with_bias, ln=None, mean=None, rstd=None):
+    """dW (N, K) = dY^T X' and db (N) = colsum dY over token rows (fixed-order, deterministic);
+    X' = LayerNorm(X) recomputed from the forward's row statistics when ln = (gamma, beta, eps)."""
+    rows = x2.shape[0]
+    dw = torch.empty(N, K, device=x2.device, dtype=torch.float32)
+    db = torch.empty(N, device=x2.device, dtype=torch.float32) if with_bias else None
+    gamma = beta = None
+    if ln is not None:
+        gamma, beta, _ = ln
+    d = _rg_desc(rows, K, N, x2.stride(0), dy2.stride(0), K, 1, ln is not None)
+    L = _lib.load()
+    ws = _workspace(L.mmni_rowgemm_dw_workspace_bytes(ctypes.byref(d)), x2.device)
+    ev = KernelTimer.start()
+    check(L.mmni_rowgemm_dw(ctypes.byref(d), ptr(x2), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), ptr(dy2), ptr(dw),
+                            ptr(db), ptr(ws), stream_handle(x2.device)), "mmni_rowgemm_dw")
+    KernelTimer.stop(f"rowgemm_dw_{N}x{K}", ev, 2.0 * rows * K * N, 4.0 * rows * (K + N))
+    return dw, db
+
+
+def row_layernorm_bwd(dxn2, x2, gamma, mean, rstd, dres2=None):
+    """dX of a LayerNorm over the C columns of token rows from dL/d(LN output) (+ dres), and
+    dgamma / dbeta (fixed-order sums)."""
+    rows, C = x2.shape
+    dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+    dgamma = torch.empty(C, device=x2.device, dtype=torch.float32)
+    dbeta = torch.empty(C, device=x2.device, dtype=torch.float32)
+    L = _lib.load()
+    ws = _workspace(L.mmni_row_layernorm_bwd_workspace_bytes(rows, C), x2.device)
+    ev = KernelTimer.start()
+    check(L.mmni_row_layernorm_bwd(rows, C, ptr(dxn2), dxn2.stride(0), ptr(x2), x2.stride(0), ptr(gamma), ptr(mean),
+                                   ptr(rstd), ptr(dres2), dres2.stride(0) if dres2 is not None else 0, ptr(dx), C,
+                                   ptr(dgamma), ptr(dbeta), ptr(ws), stream_handle(x2.device)),
+          "mmni_row_layernorm_bwd")
+    KernelTimer.stop(f"row_ln_bwd_C{C}", ev, 10.0 * rows * C, 4.0 * rows * C * (4 if dres2 is not None else 3))
+    return dx, dgamma, dbeta
+
+
+class _RowLnLinear(torch.autograd.Function):
+    """y = LayerNorm(x) W^T + b on token rows (layer_norms[0] -> in_proj slice,
+    crossmodal_transformer.py:145,150-151 + multihead_attention.py:71-84): one launch; the LN
+    output is recomputed in the backward from the saved row statistics."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w, b, eps):
+        E = x.shape[-1]
+        x2 = _rows_view(x, E).contiguous()
+        y, mean, rstd = rowgemm(x2, w, b, ln=(gamma, beta, eps), stats=True)
+        ctx.save_for_backward(x2, gamma, beta, w, mean, rstd)
+        ctx.eps, ctx.has_b, ctx.xshape = eps, b is not None, x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gamma, beta, w, mean, rstd = ctx.saved_tensors
+        N, K = w.shape
+        dy2 = _rows_view(dy, N).contiguous()
+        ln = (gamma, beta, ctx.eps)
+        dw, db = rowgemm_dw(x2, dy2, N, K, ctx.has_b, ln=ln, mean=mean, rstd=rstd)
+        dxn = rowgemm(dy2, w, transpose_w=True)
+        dx, dgamma, dbeta = row_layernorm_bwd(dxn, x2, gamma, mean, rstd)
+        return dx.view(ctx.xshape), dgamma, dbeta, dw, db, None
+
+
+class _RowLinearResidual(torch.autograd.Function):
+    """y = res + x W^T + b on token rows (out_proj + the residual add,
+    multihead_attention.py:129, crossmodal_transformer.py:153-154)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res):
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = _rows_view(x, K).contiguous()
+        r2 = _rows_view(res, N).contiguous()
+        y = rowgemm(x2, w, b, res=r2)
+        ctx.save_for_backward(x2, w)
+        ctx.has_b, ctx.xshape = b is not None, x.shape
+        return y.view(*res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        N, K = w.shape
+        dy2 = _rows_view(dy, N).contiguous()
+        dw, db = rowgemm_dw(x2, dy2, N, K, ctx.has_b)
+        dx = rowgemm(dy2, w, transpose_w=True)
+        return dx.view(ctx.xshape), dw, db, dy
+
+
+class _RowLnFfn(torch.autograd.Function):
+    """y = x + fc2(ReLU(fc1(LayerNorm(x)))) on token rows (crossmodal_transformer.py:155-165) in two
+    launches (LN + fc1 + bias + ReLU; fc2 + bias + residual); the ReLU output (rows, 4E) is kept for
+    the backward, whose ReLU mask is its sign."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w1, b1, w2, b2, eps):
+        E = x.shape[-1]
+        x2 = _rows_view(x, E).contiguous()
+        a, mean, rstd = rowgemm(x2, w1, b1, ln=(gamma, beta, eps), relu=True, stats=True)
+        y = rowgemm(a, w2, b2, res=x2)
+        ctx.save_for_backward(x2, gamma, beta, w1, w2, a, mean, rstd)
+        ctx.eps, ctx.has_b, ctx.xshape = eps, (b1 is not None, b2 is not None), x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gamma, beta, w1, w2, a, mean, rstd = ctx.saved_tensors
+        H, E = w1.shape
+        dy2 = _rows_view(dy, E).contiguous()
+        dw2, db2 = rowgemm_dw(a, dy2, E, H, ctx.has_b[1])
+        dh = rowgemm(dy2, w2, transpose_w=True, aux=a)          # (dY W2) * (a > 0)
+        ln = (gamma, beta, ctx.eps)
+        dw1, db1 = rowgemm_dw(x2, dh, H, E, ctx.has_b[0], ln=ln, mean=mean, rstd=rstd)
+        dxn = rowgemm(dh, w1, transpose_w=True)
+        dx, dgamma, dbeta = row_layernorm_bwd(dxn, x2, gamma, mean, rstd, dres2=dy2)
+        return dx.view(ctx.xshape), dgamma, dbeta, dw1, db1, dw2, db2, None
+
+
+class _MHARows(torch.autograd.Function):
+    """The fused attention core on projections that stay packed: self attention reads q / k / v as
+    column slices of one (T*B, 3E) qkv tensor, cross attention q (T*B, E) and k / v as slices of a
+    (Tk*B, 2E) kv tensor; the backward writes dq / dk / dv straight into the packed gradients
+    (the kernels take row strides), so no slice copies or gradient scatter run in between."""
+
+    @staticmethod
+    def forward(ctx, q_src, kv_src, Tq, Tk, B, heads, diag, scale, dropout, seed):
+        packed = q_src is kv_src
+        E = q_src.shape[-1] // 3 if packed else q_src.shape[-1]
+        qs = q_src.stride(0)
+        if packed:
+            q, k, v = q_src, q_src[:, E:], q_src[:, 2 * E:]
+            ks = vs = qs
+        else:
+            q, k, v = q_src, kv_src, kv_src[:, E:]
+            ks = vs = kv_src.stride(0)
+        out = torch.empty((Tq, B, E), device=q_src.device, dtype=torch.float32)
+        lse = torch.empty((B, heads, Tq), device=q_src.device, dtype=torch.float32)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed)
+        lib = _lib.load()
+        ws = _workspace(lib.mmni_mha_fwd_workspace_bytes(d), q_src.device)
+        ev = KernelTimer.start()
+        check(lib.mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse), ptr(ws), stream_handle(q_src.device)),
+              "mmni_mha_fwd")
+        KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
+        ctx.save_for_backward(q_src, kv_src, out, lse)
+        ctx.cfg = (Tq, Tk, B, heads, diag, scale, dropout, seed, packed, E, qs, ks, vs)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q_src, kv_src, out, lse = ctx.saved_tensors
+        Tq, Tk, B, heads, diag, scale, dropout, seed, packed, E, qs, ks, vs = ctx.cfg
+        dout = dout.contiguous()
+        dq_src = torch.empty_like(q_src)
+        if packed:
+            q, k, v = q_src, q_src[:, E:], q_src[:, 2 * E:]
+            dq, dk, dv = dq_src, dq_src[:, E:], dq_src[:, 2 * E:]
+            dkv_src = None
+        else:
+            dkv_src = torch.empty_like(kv_src)
+            q, k, v = q_src, kv_src, kv_src[:, E:]
+            dq, dk, dv = dq_src, dkv_src, dkv_src[:, E:]
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed)
+        lib = _lib.load()
+        ws = _workspace(lib.mmni_mha_bwd_workspace_bytes(d), q_src.device)
+        ev = KernelTimer.start()
+        check(lib.mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv),
+                               ptr(ws), stream_handle(q_src.device)), "mmni_mha_bwd")
+        KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
+        return dq_src, dkv_src, None, None, None, None, None, None, None, None
+
+
+def encoder_layer_rows(x, x_kv, layer, diag, dropout_p, seed):
+    """One pre-norm TransformerEncoderLayer (crossmodal_transformer.py:133-165) on the HIP kernels:
+    LN0 + in_proj (q | kv, or qkv for self attention) -> fused attention core -> out_proj +
+    residual -> LN1 + fc1 + ReLU -> fc2 + residual.  x (T, B, E); x_kv (Tk, B, E) shared by key and
+    value (the encoder passes the same embedded tensor for both), or None for self attention.
+    Residual / ReLU dropouts must be inactive (the caller checks)."""
+    attn = layer.self_attn
+    E = x.shape[-1]
+    Tq, B = x.shape[0], x.shape[1]
+    ln0, ln1 = layer.layer_norms[0], layer.layer_norms[1]
+    W, bW = attn.in_proj_weight, attn.in_proj_bias
+    if x_kv is None:
+        qkv = _RowLnLinear.apply(x, ln0.weight, ln0.bias, W, bW, float(ln0.eps)).view(-1, 3 * E)
+        q_src = kv_src = qkv
+        Tk = Tq
+    else:
+        q_src = _RowLnLinear.apply(x, ln0.weight, ln0.bias, W[:E], bW[:E] if bW is not None else None,
+                                   float(ln0.eps)).view(-1, E)
+        kv_src = _RowLnLinear.apply(x_kv, ln0.weight, ln0.bias, W[E:], bW[E:] if bW is not None else None,
+                                    float(ln0.eps)).view(-1, 2 * E)
+        Tk = x_kv.shape[0]
+    a = _MHARows.apply(q_src, kv_src, Tq, Tk, B, attn.num_heads_mult, diag, attn.scaling, dropout_p, seed)
+    x = _RowLinearResidual.apply(a, attn.out_proj.weight, attn.out_proj.bias, x)
+    return _RowLnFfn.apply(x, ln1.weight, ln1.bias, layer.fc1.weight, layer.fc1.bias, layer.fc2.weight,
+                           layer.fc2.bias, float(ln1.eps))

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from .position_embedding import SinusoidalPositionalEmbedding
 from .multihead_attention import MultiheadAttention
-from ..functional import SplitKLinear
+from ..functional import SplitKLinear, dropout_seed, encoder_layer_rows
 
 
 class TransformerEncoder(nn.Module):
@@ -49,7 +49,11 @@ class TransformerEncoder(nn.Module):
         cross = x_in_k is not None and x_in_v is not None
         if cross:
             x_k = self._embed(x_in_k)
-            x_v = self._embed(x_in_v)
+            # the callers pass one tensor as key and value input (model.py:489-490); its two
+            # embeddings are then equal unless dropout draws two masks, so compute it once and
+            # let the layers project key and value from one LayerNorm (identical values)
+            same = x_in_v is x_in_k and (self.dropout == 0.0 or not self.training)
+            x_v = x_k if same else self._embed(x_in_v)
         for layer in self.layers:
             x = layer(x, x_k, x_v) if cross else layer(x)
         if self.normalize:
@@ -80,7 +84,22 @@ class TransformerEncoderLayer(nn.Module):
         self.fc2 = Linear(4 * self.embed_dim, self.embed_dim)
         self.layer_norms = nn.ModuleList([LayerNorm(self.embed_dim) for _ in range(2)])
 
+    def _fused_ok(self, x, x_k, x_v):
+        inactive = lambda p: p == 0.0 or not self.training  # noqa: E731
+        return (x.is_cuda and x.dtype == torch.float32 and not torch.is_autocast_enabled()
+                and self.normalize_before and inactive(self.relu_dropout) and inactive(self.res_dropout)
+                and (x_k is None and x_v is None or x_k is x_v) and self.embed_dim <= 256
+                and self.embed_dim % self.num_heads_mult == 0 and self.embed_dim // self.num_heads_mult <= 16
+                and self.self_attn.in_proj_bias is not None and self.self_attn.bias_k is None
+                and not self.self_attn.add_zero_attn)
+
     def forward(self, x, x_k=None, x_v=None):
+        if self._fused_ok(x, x_k, x_v):
+            # HIP row-GEMM path (functional.encoder_layer_rows): LN0 + in_proj, attention core,
+            # out_proj + residual, LN1 + fc1 + ReLU, fc2 + residual in 6 launches
+            diag = (buffered_future_mask(x, x_k)._mmni_causal_diag if self.attn_mask else 0)
+            p = float(self.self_attn.attn_dropout) if self.training else 0.0
+            return encoder_layer_rows(x, x_k, self, diag, p, dropout_seed() if p > 0 else 0)
         residual = x
         x = self.maybe_layer_norm(0, x, before=True)
         mask = buffered_future_mask(x, x_k) if self.attn_mask else None

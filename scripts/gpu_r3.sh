@@ -41,6 +41,20 @@ print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_
 k=sorted(d['kernels'].items(), key=lambda kv: -kv[1]['total_ms'])[:8]; print(k)" ; tail -2 gpurun_out/bench_$TAG.err
   fatal $rc && exit $rc
 fi
+if has benchc4; then
+  timeout -k 10 600 python bench.py --config c4 --steps 10 --warmup 3 > gpurun_out/bench_c4_$TAG.json 2> gpurun_out/bench_c4_$TAG.err
+  rc=$?; echo "bench c4 rc=$rc"; python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_c4_$TAG.json').read().strip().splitlines()[-1])
+print(d['value'], d['ms_per_step'], d['config'].get('graph'), d['roofline']['kernel'], d['roofline']['avg_ms'])" ; tail -2 gpurun_out/bench_c4_$TAG.err
+  fatal $rc && exit $rc
+fi
+if has benchc5; then
+  timeout -k 10 600 python bench.py --config c5 --steps 10 --warmup 3 > gpurun_out/bench_c5_$TAG.json 2> gpurun_out/bench_c5_$TAG.err
+  rc=$?; echo "bench c5 rc=$rc"; python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_c5_$TAG.json').read().strip().splitlines()[-1])
+print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_ms'])" ; tail -2 gpurun_out/bench_c5_$TAG.err
+  fatal $rc && exit $rc
+fi
 if has profc4; then
   R="$GRAFT_REPO_ROOT"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof_c4_$TAG" -o k -- \
