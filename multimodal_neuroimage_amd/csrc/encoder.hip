@@ -25,10 +25,18 @@ namespace enc {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, BK = 32;
-constexpr int LDW = BK + 2;   // LDS row stride in floats: t * 34 + g hits 32 distinct banks per 32 lanes
-
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f4 zero4() { return (f4){0.f, 0.f, 0.f, 0.f}; }
+
+// Contraction order.  The sum over k is order-free between the operands, so k-step s of the
+// MFMA takes k = 16 (s / 4) + 4 g + (s % 4) on lane group g: the four k-steps of group j = s / 4
+// are one 16-byte piece k = 16 j + 4 g .. + 3 of a lane's row, loaded straight from global memory
+// (L2-resident weights and activations) with no LDS staging and no barriers.  Per wave a 32 x 32
+// output tile (2 x 2 MFMA tiles, four independent accumulator chains); a 256-thread block 64 x 64.
+constexpr int BM = 64, BN = 64;
+constexpr int KG = 16;       // k per group (4 k-steps)
+constexpr int KMAX_LN = 176; // LN prologue: the whole row (K <= 176, 11 groups) held in registers
+constexpr int DEPTH = 4;     // groups in flight
 
 struct RGArgs {
     int64_t rows, ldx, ldy, ldres, ldaux, w_sn, w_sk;
@@ -46,146 +54,157 @@ struct RGArgs {
     float* rstd;
 };
 
-// LayerNorm statistics (nn.LayerNorm: biased variance, eps inside the root) of the block's 64
-// rows, 4 threads per row, two passes over the row (mean, then centred squares).
-__device__ __forceinline__ void block_row_stats(const RGArgs& a, int64_t r0, float* mean_s, float* rstd_s) {
-    const int tid = threadIdx.x, rr = tid >> 2, q = tid & 3;
-    const int64_t r = r0 + rr;
-    const float* xr = a.x + r * a.ldx;
-    float s = 0.f;
-    if (r < a.rows)
-        for (int k = q; k < a.K; k += 4) s += xr[k];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    const float mean = s / (float)a.K;
-    float v = 0.f;
-    if (r < a.rows)
-        for (int k = q; k < a.K; k += 4) {
-            const float d = xr[k] - mean;
-            v = fmaf(d, d, v);
-        }
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    const float rstd = 1.0f / sqrtf(v / (float)a.K + a.eps);
-    if (q == 0) {
-        mean_s[rr] = mean;
-        rstd_s[rr] = rstd;
-        if (a.mean != nullptr && blockIdx.y == 0 && r < a.rows) {
-            a.mean[r] = mean;
-            a.rstd[r] = rstd;
-        }
-    }
+// 4 consecutive k (from k0) of row r of a (rows, ld) matrix; zeros past K / past the rows
+__device__ __forceinline__ f4 load_k4(const float* base, int64_t r, int64_t ld, bool rok, int k0, int K) {
+    const float* p = base + r * ld + k0;
+    if (rok && k0 + 3 < K && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) return *reinterpret_cast<const f4*>(p);
+    f4 v = zero4();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (rok && k0 + i < K) ? p[i] : 0.f;
+    return v;
 }
 
-// One K chunk of the block's operands into registers: 8 x-values and 8 w-values per thread.
-// x: thread -> row tid / 4, columns 8 (tid % 4) .. +7 of the chunk.  w: thread -> output n,
-// 8 consecutive k (k-contiguous weights) or output group / k (n-contiguous, the transposed use).
-struct Chunk {
-    float x[8], w[8];
-};
-
-__device__ __forceinline__ void load_chunk(const RGArgs& a, int64_t r0, int n0, int k0, Chunk& c) {
-    const int tid = threadIdx.x;
-    {
-        const int rr = tid >> 2, kk = (tid & 3) * 8;
-        const int64_t r = r0 + rr;
-        const float* xr = a.x + r * a.ldx + k0 + kk;
+// W(n, k0 .. k0 + 3): k-contiguous (w_sk = 1) as a 16-byte piece, n-contiguous (the transpose) as
+// four scalars of rows k0 .. k0 + 3 (lanes of a group read 16 consecutive n: coalesced)
+__device__ __forceinline__ f4 load_w4(const RGArgs& a, int n, int k0) {
+    const bool nok = n < a.N;
+    if (a.w_sk == 1) return load_k4(a.w, n, a.w_sn, nok, k0, a.K);
+    f4 v = zero4();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) c.x[j] = (r < a.rows && k0 + kk + j < a.K) ? xr[j] : 0.f;
-    }
-    if (a.w_sk == 1) {   // W rows along k: thread -> n = tid / 4, 8 consecutive k
-        const int nn = tid >> 2, kk = (tid & 3) * 8;
-        const int n = n0 + nn;
-        const float* wr = a.w + (int64_t)n * a.w_sn + k0 + kk;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) c.w[j] = (n < a.N && k0 + kk + j < a.K) ? wr[j] : 0.f;
-    } else {             // W columns along n (w_sn == 1): thread -> k = tid / 8, 8 consecutive n
-        const int kk = tid >> 3, nn = (tid & 7) * 8;
-        const int k = k0 + kk;
-        const float* wr = a.w + (int64_t)k * a.w_sk + n0 + nn;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) c.w[j] = (k < a.K && n0 + nn + j < a.N) ? wr[j] : 0.f;
-    }
+    for (int i = 0; i < 4; ++i) v[i] = (nok && k0 + i < a.K) ? a.w[(int64_t)(k0 + i) * a.w_sk + n] : 0.f;
+    return v;
 }
 
-__device__ __forceinline__ void store_chunk(const RGArgs& a, int k0, const Chunk& c, float (*xs)[LDW],
-                                            float (*ws)[LDW], const float* mean_s, const float* rstd_s) {
-    const int tid = threadIdx.x;
-    {
-        const int rr = tid >> 2, kk = (tid & 3) * 8;
-        if (a.ln) {
-            const float m = mean_s[rr], rs = rstd_s[rr];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = k0 + kk + j;
-                xs[rr][kk + j] = k < a.K ? fmaf((c.x[j] - m) * rs, a.gamma[k], a.beta[k]) : 0.f;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xs[rr][kk + j] = c.x[j];
-        }
-    }
-    if (a.w_sk == 1) {
-        const int nn = tid >> 2, kk = (tid & 3) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ws[nn][kk + j] = c.w[j];
-    } else {
-        const int kk = tid >> 3, nn = (tid & 7) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ws[nn + j][kk] = c.w[j];
-    }
-}
-
+template <bool LN>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
-    __shared__ float xs[BM][LDW];
-    __shared__ float ws[BN][LDW];
-    __shared__ float mean_s[BM], rstd_s[BM];
-    const int64_t r0 = (int64_t)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t = lane & 15, g = lane >> 4;
-    const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
-    if (a.ln) block_row_stats(a, r0, mean_s, rstd_s);
+    const int64_t m0 = (int64_t)blockIdx.x * BM + (wave & 1) * 32;     // the wave's 32 rows
+    const int n0 = blockIdx.y * BN + (wave >> 1) * 32;                 // and 32 outputs
+    const int64_t ra = m0 + t, rb = m0 + 16 + t;                       // A rows of the two m tiles
+    const bool oka = ra < a.rows, okb = rb < a.rows;
+    const int na = n0 + t, nb = n0 + 16 + t;                           // B columns of the two n tiles
+    const int NG = (a.K + KG - 1) / KG;
     f4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
-    Chunk cur;
-    load_chunk(a, r0, n0, 0, cur);
-    for (int k0 = 0; k0 < a.K; k0 += BK) {
-        __syncthreads();   // previous chunk's MFMA reads done (and the row statistics, first time)
-        store_chunk(a, k0, cur, xs, ws, mean_s, rstd_s);
-        __syncthreads();
-        if (k0 + BK < a.K) load_chunk(a, r0, n0, k0 + BK, cur);   // in flight during the MFMAs
-        const int rem = a.K - k0 < BK ? a.K - k0 : BK;
-        const int ks = (rem + 3) / 4;   // k-steps of this chunk (columns past K are zero)
-        auto step = [&](int s) {
-            const float x0 = xs[wm + t][4 * s + g], x1 = xs[wm + 16 + t][4 * s + g];
-            const float w0 = ws[wn + t][4 * s + g], w1 = ws[wn + 16 + t][4 * s + g];
-            acc[0][0] = mfma(x0, w0, acc[0][0]);
-            acc[0][1] = mfma(x0, w1, acc[0][1]);
-            acc[1][0] = mfma(x1, w0, acc[1][0]);
-            acc[1][1] = mfma(x1, w1, acc[1][1]);
-        };
-        if (ks == BK / 4) {
+        for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+    auto mma_group = [&](f4 xa, f4 xb, f4 wa, f4 wb) {
 #pragma unroll
-            for (int s = 0; s < BK / 4; ++s) step(s);
-        } else {
-            for (int s = 0; s < ks; ++s) step(s);
+        for (int i = 0; i < 4; ++i) {
+            acc[0][0] = mfma(xa[i], wa[i], acc[0][0]);
+            acc[0][1] = mfma(xa[i], wb[i], acc[0][1]);
+            acc[1][0] = mfma(xb[i], wa[i], acc[1][0]);
+            acc[1][1] = mfma(xb[i], wb[i], acc[1][1]);
+        }
+    };
+    if constexpr (LN) {
+        // the two rows' whole K extent in registers, LayerNorm statistics by the 4 lane groups
+        constexpr int MG = KMAX_LN / KG;
+        f4 xa[MG], xb[MG];
+#pragma unroll
+        for (int j = 0; j < MG; ++j) {
+            if (j < NG) {
+                xa[j] = load_k4(a.x, ra, a.ldx, oka, KG * j + 4 * g, a.K);
+                xb[j] = load_k4(a.x, rb, a.ldx, okb, KG * j + 4 * g, a.K);
+            } else {
+                xa[j] = xb[j] = zero4();
+            }
+        }
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int j = 0; j < MG; ++j) {
+            sa += (xa[j][0] + xa[j][1]) + (xa[j][2] + xa[j][3]);
+            sb += (xb[j][0] + xb[j][1]) + (xb[j][2] + xb[j][3]);
+        }
+        sa += __shfl_xor(sa, 16); sa += __shfl_xor(sa, 32);
+        sb += __shfl_xor(sb, 16); sb += __shfl_xor(sb, 32);
+        const float invK = 1.0f / (float)a.K;
+        const float ma = sa * invK, mb = sb * invK;
+        float va = 0.f, vb = 0.f;
+#pragma unroll
+        for (int j = 0; j < MG; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool in = KG * j + 4 * g + i < a.K;
+                const float da = in ? xa[j][i] - ma : 0.f, db = in ? xb[j][i] - mb : 0.f;
+                va = fmaf(da, da, va);
+                vb = fmaf(db, db, vb);
+            }
+        va += __shfl_xor(va, 16); va += __shfl_xor(va, 32);
+        vb += __shfl_xor(vb, 16); vb += __shfl_xor(vb, 32);
+        const float rsa = 1.0f / sqrtf(va * invK + a.eps), rsb = 1.0f / sqrtf(vb * invK + a.eps);
+        if (a.mean != nullptr && blockIdx.y == 0 && (wave >> 1) == 0 && g == 0) {
+            if (oka) { a.mean[ra] = ma; a.rstd[ra] = rsa; }
+            if (okb) { a.mean[rb] = mb; a.rstd[rb] = rsb; }
+        }
+        f4 wa[DEPTH], wb[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            wa[d] = d < NG ? load_w4(a, na, KG * d + 4 * g) : zero4();
+            wb[d] = d < NG ? load_w4(a, nb, KG * d + 4 * g) : zero4();
+        }
+#pragma unroll
+        for (int j = 0; j < MG; ++j) {
+            if (j < NG) {
+            f4 ga, gb, xna, xnb;
+            const int k0 = KG * j + 4 * g;
+            ga = load_k4(a.gamma, 0, 0, true, k0, a.K);
+            gb = load_k4(a.beta, 0, 0, true, k0, a.K);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xna[i] = fmaf((xa[j][i] - ma) * rsa, ga[i], gb[i]);
+                xnb[i] = fmaf((xb[j][i] - mb) * rsb, ga[i], gb[i]);
+            }
+            const f4 wcur_a = wa[j % DEPTH], wcur_b = wb[j % DEPTH];
+            if (j + DEPTH < NG) {
+                wa[j % DEPTH] = load_w4(a, na, KG * (j + DEPTH) + 4 * g);
+                wb[j % DEPTH] = load_w4(a, nb, KG * (j + DEPTH) + 4 * g);
+            }
+            mma_group(xna, xnb, wcur_a, wcur_b);
+            }
+        }
+    } else {
+        // stream K in groups, DEPTH groups of all four operands in flight
+        f4 xa[DEPTH], xb[DEPTH], wa[DEPTH], wb[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const int k0 = KG * d + 4 * g;
+            const bool v = d < NG;
+            xa[d] = v ? load_k4(a.x, ra, a.ldx, oka, k0, a.K) : zero4();
+            xb[d] = v ? load_k4(a.x, rb, a.ldx, okb, k0, a.K) : zero4();
+            wa[d] = v ? load_w4(a, na, k0) : zero4();
+            wb[d] = v ? load_w4(a, nb, k0) : zero4();
+        }
+        for (int j0 = 0; j0 < NG; j0 += DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+                const int j = j0 + d;
+                if (j >= NG) break;
+                const f4 ca = xa[d], cb = xb[d], cwa = wa[d], cwb = wb[d];
+                if (j + DEPTH < NG) {
+                    const int k0 = KG * (j + DEPTH) + 4 * g;
+                    xa[d] = load_k4(a.x, ra, a.ldx, oka, k0, a.K);
+                    xb[d] = load_k4(a.x, rb, a.ldx, okb, k0, a.K);
+                    wa[d] = load_w4(a, na, k0);
+                    wb[d] = load_w4(a, nb, k0);
+                }
+                mma_group(ca, cb, cwa, cwb);
+            }
         }
     }
     // epilogue: D[row 4 g + i][col t] of tile (mi, ni)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-        const int n = n0 + wn + 16 * ni + t;
+        const int n = n0 + 16 * ni + t;
         if (n >= a.N) continue;
         const float b = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int64_t r = r0 + wm + 16 * mi + 4 * g + i;
+                const int64_t r = m0 + 16 * mi + 4 * g + i;
                 if (r >= a.rows) continue;
                 float v = acc[mi][ni][i] + b;
                 if (a.relu) v = fmaxf(v, 0.f);
@@ -199,6 +218,7 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // weight gradient: dW[n][k] = sum_r dY[r][n] X'[r][k] (+ db[n] as the extra column k = K of ones)
+// per (64 x 64 output tile, row chunk) block; partials [chunk][N * K + N] reduced in chunk order
 // ---------------------------------------------------------------------------------------------
 struct DWArgs {
     int64_t rows, ldx, lddy;
@@ -212,54 +232,74 @@ struct DWArgs {
     float* part;   // [chunk][N * K + N]: dW row-major, then db
 };
 
-constexpr int DR = 32;   // rows staged per LDS round
+// rows r0 + 16 j + 4 g + i (i = 0..3) of column c (scalars; the 16 lanes of a group read 16
+// consecutive columns of each row)
+__device__ __forceinline__ f4 load_rows4(const float* base, int64_t ld, int64_t r0, int64_t rend, int c, int C) {
+    f4 v = zero4();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (r0 + i < rend && c < C) ? base[(r0 + i) * ld + c] : 0.f;
+    return v;
+}
 
 __global__ __launch_bounds__(256) void rowgemm_dw_kernel(DWArgs a) {
-    // block: outputs n0..n0+63 x k0..k0+63 (k = K is the ones column), rows of chunk blockIdx.z
-    // row stride 80 floats: lanes (t, g) reading [4 s + g][t] hit banks 16 g + t, all distinct
-    __shared__ float ds[DR][BN + 16];   // dY[r][n]
-    __shared__ float xs[DR][BN + 16];   // X'[r][k]
-    const int n0 = blockIdx.x * BN, k0 = blockIdx.y * BN;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int t = lane & 15, g = lane >> 4;
+    const int n0 = blockIdx.x * BN + (wave & 1) * 32, k0 = blockIdx.y * BN + (wave >> 1) * 32;
     const int64_t rbeg = (int64_t)blockIdx.z * a.rows_per_chunk;
     const int64_t rend = rbeg + a.rows_per_chunk < a.rows ? rbeg + a.rows_per_chunk : a.rows;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = lane & 15, g = lane >> 4;
-    const int wn = (wave & 1) * 32, wk = (wave >> 1) * 32;
+    const int na = n0 + t, nb = n0 + 16 + t, ka = k0 + t, kb = k0 + 16 + t;
     f4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
-    for (int64_t rb = rbeg; rb < rend; rb += DR) {
-        __syncthreads();
-        // stage DR rows x 64 columns of dY and X' (thread -> row tid / 8, 8 consecutive columns)
-        const int rr = tid >> 3, cc = (tid & 7) * 8;
-        const int64_t r = rb + rr;
-        const bool rok = r < rend;
+        for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+    // X' column k of rows r..r+3: LayerNorm recompute, the ones column k == K (db), zeros past it
+    auto load_x = [&](int64_t r, int k) {
+        f4 v = zero4();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int n = n0 + cc + j;
-            ds[rr][cc + j] = (rok && n < a.N) ? a.dy[r * a.lddy + n] : 0.f;
-            const int k = k0 + cc + j;
-            float xv = 0.f;
-            if (rok && k < a.K) {
-                xv = a.x[r * a.ldx + k];
-                if (a.ln) xv = fmaf((xv - a.mean[r]) * a.rstd[r], a.gamma[k], a.beta[k]);
-            } else if (rok && k == a.K) {
-                xv = 1.0f;   // db
+        for (int i = 0; i < 4; ++i) {
+            const int64_t rr = r + i;
+            if (rr < rend && k < a.K) {
+                float xv = a.x[rr * a.ldx + k];
+                if (a.ln) xv = fmaf((xv - a.mean[rr]) * a.rstd[rr], a.gamma[k], a.beta[k]);
+                v[i] = xv;
+            } else if (rr < rend && k == a.K) {
+                v[i] = 1.0f;
             }
-            xs[rr][cc + j] = xv;
         }
-        __syncthreads();
+        return v;
+    };
+    const int NG = (int)((rend - rbeg + KG - 1) / KG);
+    f4 da[DEPTH], db[DEPTH], xa[DEPTH], xb[DEPTH];
 #pragma unroll
-        for (int s = 0; s < DR / 4; ++s) {
-            // A[row n = t][kk = row g]: dY[4 s + g][n]; B[kk = row g][col k = t]: X'[4 s + g][k]
-            const float d0 = ds[4 * s + g][wn + t], d1 = ds[4 * s + g][wn + 16 + t];
-            const float x0 = xs[4 * s + g][wk + t], x1 = xs[4 * s + g][wk + 16 + t];
-            acc[0][0] = mfma(d0, x0, acc[0][0]);
-            acc[0][1] = mfma(d0, x1, acc[0][1]);
-            acc[1][0] = mfma(d1, x0, acc[1][0]);
-            acc[1][1] = mfma(d1, x1, acc[1][1]);
+    for (int d = 0; d < DEPTH; ++d) {
+        const int64_t r = rbeg + KG * d + 4 * g;
+        da[d] = load_rows4(a.dy, a.lddy, r, rend, na, a.N);
+        db[d] = load_rows4(a.dy, a.lddy, r, rend, nb, a.N);
+        xa[d] = load_x(r, ka);
+        xb[d] = load_x(r, kb);
+    }
+    for (int j0 = 0; j0 < NG; j0 += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const int j = j0 + d;
+            if (j >= NG) break;
+            const f4 ca = da[d], cb = db[d], cxa = xa[d], cxb = xb[d];
+            if (j + DEPTH < NG) {
+                const int64_t r = rbeg + KG * (j + DEPTH) + 4 * g;
+                da[d] = load_rows4(a.dy, a.lddy, r, rend, na, a.N);
+                db[d] = load_rows4(a.dy, a.lddy, r, rend, nb, a.N);
+                xa[d] = load_x(r, ka);
+                xb[d] = load_x(r, kb);
+            }
+            // A[row n][kk = row]: dY;  B[kk = row][col k]: X'
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                acc[0][0] = mfma(ca[i], cxa[i], acc[0][0]);
+                acc[0][1] = mfma(ca[i], cxb[i], acc[0][1]);
+                acc[1][0] = mfma(cb[i], cxa[i], acc[1][0]);
+                acc[1][1] = mfma(cb[i], cxb[i], acc[1][1]);
+            }
         }
     }
     // D[row n = 4 g + i][col k = t]
@@ -268,15 +308,48 @@ __global__ __launch_bounds__(256) void rowgemm_dw_kernel(DWArgs a) {
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
         for (int ki = 0; ki < 2; ++ki) {
-            const int k = k0 + wk + 16 * ki + t;
+            const int k = k0 + 16 * ki + t;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int n = n0 + wn + 16 * ni + 4 * g + i;
+                const int n = n0 + 16 * ni + 4 * g + i;
                 if (n >= a.N) continue;
                 if (k < a.K) p[(int64_t)n * a.K + k] = acc[ni][ki][i];
                 else if (k == a.K) p[(int64_t)a.N * a.K + n] = acc[ni][ki][i];
             }
         }
+}
+
+// out[j] = sum_c part[c][j] in chunk order (deterministic); columns [0, split) -> out, [split, ncols)
+// -> out2 (nullable).  One thread per 4 columns, every chunk's load issued before the adds.
+__global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ part, int nchunks, int ncols,
+                                                        int split, float* out, float* out2) {
+    const int j4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (j4 >= ncols) return;
+    f4 s = zero4();
+    const bool vec = j4 + 3 < ncols && (ncols & 3) == 0;
+    for (int c0 = 0; c0 < nchunks; c0 += 8) {
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            v[u] = zero4();
+            if (c0 + u < nchunks) {
+                const float* p = part + (int64_t)(c0 + u) * ncols + j4;
+                if (vec) v[u] = *reinterpret_cast<const f4*>(p);
+                else
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[u][i] = j4 + i < ncols ? p[i] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = j4 + i;
+        if (j >= ncols) break;
+        if (j < split) out[j] = s[i];
+        else if (out2 != nullptr) out2[j - split] = s[i];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -347,14 +420,22 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
     }
 }
 
-constexpr int kLnbBlocks = 512;
+constexpr int kLnbBlocks = 128;
 
-int dw_chunks(int64_t rows) {
-    // >= 256 rows per chunk, at most 64 chunks: the partial slab stays small and the column sum short
-    int64_t c = rows / 256;
-    if (c > 64) c = 64;
+// row chunks of a weight gradient: >= 64 rows each (4 groups per wave), at most 256, and a
+// partial slab of at most 8 MB (the chunk-order reduction reads it once)
+int dw_chunks(int64_t rows, int N, int K) {
+    int64_t c = rows / 64;
+    const int64_t cap = (int64_t)(8 << 20) / (((int64_t)N * K + N) * 4);
+    if (c > cap) c = cap;
+    if (c > 256) c = 256;
     if (c < 1) c = 1;
     return (int)c;
+}
+
+void chunk_sum(const float* part, int nchunks, int ncols, int split, float* out, float* out2, hipStream_t s) {
+    const int threads = (ncols + 3) / 4;
+    chunk_sum_kernel<<<(threads + 255) / 256, 256, 0, s>>>(part, nchunks, ncols, split, out, out2);
 }
 
 }  // namespace enc
@@ -373,6 +454,8 @@ extern "C" int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const fl
                    "rowgemm: weight must be k-contiguous (w_sk = 1) or n-contiguous (w_sn = 1)");
     MMNI_ARG_CHECK(!d->ln || (gamma && beta), "rowgemm: LayerNorm prologue needs gamma and beta");
     MMNI_ARG_CHECK(!d->ln || ((mean == nullptr) == (rstd == nullptr)), "rowgemm: mean and rstd go together");
+    MMNI_ARG_CHECK(!d->ln || d->K <= enc::KMAX_LN, "rowgemm: LayerNorm prologue over K=%d > %d columns", d->K,
+                   enc::KMAX_LN);
     MMNI_ARG_CHECK(aux == nullptr || d->ldaux >= d->N, "rowgemm: aux leading dimension below N");
     MMNI_ARG_CHECK(res == nullptr || d->ldres >= d->N, "rowgemm: residual leading dimension below N");
     enc::RGArgs a{};
@@ -381,13 +464,14 @@ extern "C" int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const fl
     a.x = x; a.gamma = gamma; a.beta = beta; a.w = w; a.bias = bias; a.aux = aux; a.res = res; a.y = y;
     a.mean = d->ln ? mean : nullptr; a.rstd = d->ln ? rstd : nullptr;
     const dim3 grid((unsigned)((d->rows + enc::BM - 1) / enc::BM), (unsigned)((d->N + enc::BN - 1) / enc::BN));
-    enc::rowgemm_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    if (d->ln) enc::rowgemm_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else enc::rowgemm_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     return launch_status("rowgemm");
 }
 
 extern "C" size_t mmni_rowgemm_dw_workspace_bytes(const mmni_rowgemm_desc* d) {
     if (d == nullptr || d->rows <= 0 || d->K <= 0 || d->N <= 0) return 0;
-    return (size_t)enc::dw_chunks(d->rows) * ((size_t)d->N * d->K + d->N) * sizeof(float);
+    return (size_t)enc::dw_chunks(d->rows, d->N, d->K) * ((size_t)d->N * d->K + d->N) * sizeof(float);
 }
 
 extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const float* gamma, const float* beta,
@@ -399,7 +483,7 @@ extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const
     MMNI_ARG_CHECK(!d->ln || (gamma && beta && mean && rstd), "rowgemm_dw: LayerNorm recompute needs its inputs");
     enc::DWArgs a{};
     a.rows = d->rows; a.ldx = d->ldx; a.lddy = d->ldy; a.K = d->K; a.N = d->N; a.ln = d->ln;
-    const int chunks = enc::dw_chunks(d->rows);
+    const int chunks = enc::dw_chunks(d->rows, d->N, d->K);
     a.rows_per_chunk = (int)((d->rows + chunks - 1) / chunks);
     a.x = x; a.gamma = gamma; a.beta = beta; a.mean = mean; a.rstd = rstd; a.dy = dy;
     a.part = static_cast<float*>(workspace);
@@ -408,14 +492,8 @@ extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const
     enc::rowgemm_dw_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a);
     int rc = launch_status("rowgemm_dw");
     if (rc) return rc;
-    ColSegs segs{};
-    segs.n = 2;
-    segs.end[0] = d->N * d->K;
-    segs.end[1] = d->N * d->K + d->N;
-    segs.dst[0] = dw;
-    segs.dst[1] = db;   // null: the bias gradient is dropped
-    segs.accumulate = 0;
-    column_sum_segs(a.part, chunks, d->N * d->K + d->N, segs, (hipStream_t)stream);
+    // dW = columns [0, N K), db = [N K, N K + N) (a null db drops them)
+    enc::chunk_sum(a.part, chunks, d->N * d->K + d->N, d->N * d->K, dw, db, (hipStream_t)stream);
     return launch_status("rowgemm_dw_sum");
 }
 
@@ -442,13 +520,6 @@ extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int
     enc::row_ln_bwd_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
     int rc = launch_status("row_layernorm_bwd");
     if (rc) return rc;
-    ColSegs segs{};
-    segs.n = 2;
-    segs.end[0] = C;
-    segs.end[1] = 2 * C;
-    segs.dst[0] = dgamma;
-    segs.dst[1] = dbeta;
-    segs.accumulate = 0;
-    column_sum_segs(a.part, (int)blocks, 2 * C, segs, (hipStream_t)stream);
+    enc::chunk_sum(a.part, (int)blocks, 2 * C, C, dgamma, dbeta, (hipStream_t)stream);
     return launch_status("row_layernorm_bwd_sum");
 }

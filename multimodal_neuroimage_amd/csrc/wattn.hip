@@ -103,8 +103,11 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_kernel(WAArgs a) {
     const int r = tid / KS, p = tid - r * KS;
     const int wl = r / N, t = r - wl * N;
     const int wl_c = wl < WPB ? wl : WPB - 1;
+    // head group blockIdx.y of a.hsplit: this block's heads h0 .. h0 + NH - 1 of NHT
+    const int NHT = NH * a.hsplit, h0 = blockIdx.y * NH;
+    a.q += h0 * HD; a.k += h0 * HD; a.v += h0 * HD; a.out += h0 * HD; a.tau += h0;
 
-    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[e] * kLog2e;
+    for (int e = tid; e < g.Tsz * NH; e += blockDim.x) tab_s[e] = a.table[(e / NH) * NHT + h0 + e % NH] * kLog2e;
 
     float tau2[NH];
 #pragma unroll
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(MAXT) void wattn_fwd_kernel(WAArgs a) {
                 const float inv = 1.0f / l[h];
 #pragma unroll
                 for (int c = 0; c < HD; ++c) o[h * HD + c] = acc[h * HD + c] * inv;
-                a.lse[row * NH + h] = (m[h] + fast_log2(l[h])) * kLn2;
+                a.lse[row * NHT + h0 + h] = (m[h] + fast_log2(l[h])) * kLn2;
             }
             store_row<C>(a.out + row * a.os, o);
         }
@@ -269,9 +272,13 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     const int wl = r / N, t = r - wl * N;
     const int wl_c = wl < WPB ? wl : WPB - 1;
     const int lane = tid & 63;
+    // head group blockIdx.y of a.hsplit: this block's heads h0 .. h0 + NH - 1 of NHT
+    const int NHT = NH * a.hsplit, h0 = blockIdx.y * NH;
+    a.q += h0 * HD; a.k += h0 * HD; a.v += h0 * HD; a.o += h0 * HD; a.dout += h0 * HD;
+    a.dq += h0 * HD; a.dk += h0 * HD; a.dv += h0 * HD; a.tau += h0;
 
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
-        tab_s[e] = a.table[e] * kLog2e;
+        tab_s[e] = a.table[(e / NH) * NHT + h0 + e % NH] * kLog2e;
         dtab_s[e] = 0ull;
     }
     const float ymul = exp2f((float)fix_exponent(a.maxbits, HD));
@@ -306,7 +313,7 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
                     aq[h * HD + c] *= t2;
                     dd = fmaf(o[h * HD + c], dO[h * HD + c], dd);
                 }
-                lse2[h] = a.lse[row * NH + h] * kLog2e;
+                lse2[h] = a.lse[row * NHT + h0 + h] * kLog2e;
                 dl[h] = dd;
             }
         } else {
@@ -506,13 +513,13 @@ __global__ __launch_bounds__(MAXT) void wattn_bwd_kernel(WAArgs a) {
     __syncthreads();
     for (int e = tid; e < g.Tsz * NH; e += blockDim.x) {
         const unsigned long long v = dtab_s[e];
-        if (v != 0ull) atomicAdd(&a.dtab_fix[e], v);
+        if (v != 0ull) atomicAdd(&a.dtab_fix[(e / NH) * NHT + h0 + e % NH], v);
     }
     if (KIND == 1 && tid < NH) {
         // dtau = sum ds * (q-hat . k-hat);  dot was taken against tau*log2e*q-hat
         float v = 0.f;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += dtau_s[w * NH + tid];
-        a.dtau_part[(size_t)blockIdx.x * NH + tid] = v / (a.tau[tid] * kLog2e);
+        a.dtau_part[(size_t)blockIdx.x * NHT + h0 + tid] = v / (a.tau[tid] * kLog2e);
     }
 }
 
@@ -613,16 +620,22 @@ static size_t wattn_lds_bytes(bool bwd, bool packed, int C, int NH, int WPB, int
 }
 
 // qpl: queries per lane (2 for wattn_fwd_pk2_kernel, forward only): a window occupies N / qpl x KS lanes.
-static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1) {
+// hs: head groups (blocks per window group, grid.y).  Small launches (few windows, e.g. the 3^3
+// and 6^3 Swin-V2 stages of C2: 4 windows) spread over the CUs: 4 key slices per row and fewer
+// windows per block, so windows x head groups make the blocks.
+static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, WAConfig& cfg, int qpl = 1,
+                int hs = 1) {
     const int chunk = packed ? (qpl >= 2 ? kPk2Chunk : kPkChunk) : CH;
     const int N = g.N, R = N / qpl;
-    int KS = qpl >= 2 ? kPk2Ks : (N >= 128 ? 4 : (N >= 32 ? 2 : 1));
+    const bool small = !packed && (int64_t)g.nwin * hs < kNumCU;
+    int KS = qpl >= 2 ? kPk2Ks : (N >= 128 || small ? 4 : (N >= 32 ? 2 : 1));
     auto r64 = [](int x) { return (x + 63) / 64 * 64; };
     while (KS > 1 && r64(R * KS) > maxt) KS >>= 1;
     MMNI_ARG_CHECK(r64(R) <= maxt, "wattn: window of %d tokens exceeds %d threads", N, maxt);
     const int target = maxt < 512 ? maxt : 512;
     int WPB = target / (R * KS);
     if (qpl == 2 && !bwd && WPB > kPk2FwdWpb) WPB = kPk2FwdWpb;
+    if (small) WPB = 1;
     if (WPB < 1) WPB = 1;
     const int NPAD = (N + KS * chunk - 1) / (KS * chunk) * (KS * chunk);
     while (WPB > 1 && wattn_lds_bytes(bwd, packed, C, NH, WPB, NPAD, g.Tsz) > 160 * 1024) --WPB;
@@ -648,9 +661,9 @@ static int plan(const WGeom& g, int C, int NH, int maxt, bool bwd, bool packed, 
     return 0;
 }
 
-static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
+// C: the channels one block attends over (d->C, or d->C / head groups for the head-split launches)
+static int dispatch(const mmni_wattn_desc* d, int C, int HD, bool bwd, void*& kf, void*& kb, int& maxt, bool& packed,
                     int& qpl) {
-    const int C = d->C;
     packed = false;
     qpl = 1;
     int mf = 0, mb = 0, qf = 1;
@@ -668,14 +681,31 @@ static int dispatch(const mmni_wattn_desc* d, int HD, bool bwd, void*& kf, void*
         return 0;                                        \
     }
     MMNI_WA_CASE(12, 2, 1024)
+    MMNI_WA_CASE(4, 4, 1024)
     MMNI_WA_CASE(12, 4, 1024)
     MMNI_WA_CASE(24, 2, 512)
     MMNI_WA_CASE(24, 4, 512)
     MMNI_WA_CASE(48, 4, 256)
     MMNI_WA_CASE(6, 2, 1024)
 #undef MMNI_WA_CASE
-    set_error("wattn: unsupported (C=%d, head_dim=%d); supported: (12,2) (12,4) (24,2) (24,4) (48,4) (6,2)", C, HD);
+    set_error("wattn: unsupported (C=%d, head_dim=%d); supported: (12,2) (4,4) (12,4) (24,2) (24,4) (48,4) (6,2)", C, HD);
     return -2;
+}
+
+// Head groups for small launches of the generic head_dim-4 kernels (Swin-V2): each block takes
+// C / hs channels (an instantiated width), so few windows still fill the chip.  The smallest split
+// that reaches kNumCU blocks, else the largest available.
+static int head_split(const WGeom& g, int C, int heads, int HD) {
+    if (HD != 4 || (int64_t)g.nwin >= kNumCU) return 1;
+    int best = 1;
+    for (int hs = 2; hs <= heads; ++hs) {
+        if (heads % hs) continue;
+        const int cs = C / hs;
+        if (cs != 4 && cs != 12 && cs != 24) continue;
+        best = hs;
+        if ((int64_t)g.nwin * hs >= kNumCU) break;
+    }
+    return best;
 }
 
 static int fill_args(const mmni_wattn_desc* d, WAArgs& a, int& HD) {
@@ -736,19 +766,20 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     int maxt;
     bool packed = false;
     int qpl = 1;
-    rc = dispatch(d, HD, false, kf, kb, maxt, packed, qpl);
+    const int hs = head_split(a.g, d->C, d->heads, HD);
+    rc = dispatch(d, d->C / hs, HD, false, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, false, packed, cfg, qpl);
+    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, false, packed, cfg, qpl, hs);
     if (rc) return rc;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.out = out; a.lse = lse;
     a.vmax = packed ? vmax : nullptr;   // the packed kernels fold max|v| into their K/V staging
-    a.hsplit = 1;
+    a.hsplit = hs;
     rc = ensure_lds_attr(kf, cfg.lds);
     if (rc) return rc;
     void* args[] = {&a};
-    hipError_t e = hipLaunchKernel(kf, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
+    hipError_t e = hipLaunchKernel(kf, dim3(cfg.grid, hs), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_fwd launch: %s", hipGetErrorString(e)); return (int)e; }
     if (vmax && !packed) {   // generic kernels: a separate pass over v (vmax is maxbits[1]-shaped: pass vmax - 1)
         const long long T = (long long)a.g.nwin * a.g.N;
@@ -797,12 +828,13 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     int maxt;
     bool packed = false;
     int qpl = 1;
-    rc = dispatch(d, HD, true, kf, kb, maxt, packed, qpl);
+    const int hs = head_split(a.g, d->C, d->heads, HD);
+    rc = dispatch(d, d->C / hs, HD, true, kf, kb, maxt, packed, qpl);
     if (rc) return rc;
     WAConfig cfg;
-    rc = plan(a.g, d->C, d->heads, maxt, true, packed, cfg, qpl);
+    rc = plan(a.g, d->C / hs, d->heads / hs, maxt, true, packed, cfg, qpl, hs);
     if (rc) return rc;
-    a.hsplit = 1;
+    a.hsplit = hs;
     a.KS = cfg.KS; a.WPB = cfg.WPB; a.NPAD = cfg.NPAD; a.ngroups = cfg.ngroups;
     a.q = q; a.k = k; a.v = v; a.table = table; a.tau = tau ? tau : table; a.lse = const_cast<float*>(lse);
     a.o = out; a.dout = dout; a.dq = dq; a.dk = dk; a.dv = dv; a.dtable = dtable; a.dtau = dtau ? dtau : dtable;
@@ -830,7 +862,7 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
     rc = launch_status("wattn_absmax");
     if (rc) return rc;
     void* args[] = {&a};
-    e = hipLaunchKernel(kb, dim3(cfg.grid), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
+    e = hipLaunchKernel(kb, dim3(cfg.grid, hs), dim3(cfg.threads), args, cfg.lds, (hipStream_t)stream);
     if (e != hipSuccess) { set_error("wattn_bwd launch: %s", hipGetErrorString(e)); return (int)e; }
     wattn_dtable_convert_kernel<<<(ntab + 255) / 256, 256, 0, (hipStream_t)stream>>>(a.dtab_fix, a.maxbits, HD,
                                                                                      a.fix_shift, dtable, ntab);

@@ -1033,12 +1033,16 @@ def rowgemm(x2, w, bias=None, *, ln=None, relu=False, aux=None, res=None, transp
     return (y, mean, rstd) if stats else y
 
 
-def rowgemm_dw(x2, dy2, N, K, with_bias, ln=None, mean=None, rstd=None):
+def rowgemm_dw(x2, dy2, N, K, with_bias, ln=None, mean=None, rstd=None, out=None):
     """dW (N, K) = dY^T X' and db (N) = colsum dY over token rows (fixed-order, deterministic);
-    X' = LayerNorm(X) recomputed from the forward's row statistics when ln = (gamma, beta, eps)."""
+    X' = LayerNorm(X) recomputed from the forward's row statistics when ln = (gamma, beta, eps).
+    out = (dw, db): contiguous destinations (e.g. row blocks of a larger weight's gradient)."""
     rows = x2.shape[0]
-    dw = torch.empty(N, K, device=x2.device, dtype=torch.float32)
-    db = torch.empty(N, device=x2.device, dtype=torch.float32) if with_bias else None
+    if out is not None:
+        dw, db = out
+    else:
+        dw = torch.empty(N, K, device=x2.device, dtype=torch.float32)
+        db = torch.empty(N, device=x2.device, dtype=torch.float32) if with_bias else None
     gamma = beta = None
     if ln is not None:
         gamma, beta, _ = ln
@@ -1070,30 +1074,70 @@ def row_layernorm_bwd(dxn2, x2, gamma, mean, rstd, dres2=None):
     return dx, dgamma, dbeta
 
 
-class _RowLnLinear(torch.autograd.Function):
-    """y = LayerNorm(x) W^T + b on token rows (layer_norms[0] -> in_proj slice,
-    crossmodal_transformer.py:145,150-151 + multihead_attention.py:71-84): one launch; the LN
-    output is recomputed in the backward from the saved row statistics."""
+class _RowLnQKV(torch.autograd.Function):
+    """LayerNorm0 + in_proj of one encoder layer (crossmodal_transformer.py:145,150-151 +
+    multihead_attention.py:71-84) on token rows, LN fused into the projection (one launch per
+    input; the LN output is recomputed in the backward from the saved row statistics).
+      self attention (x_kv None): qkv = LN(x) W^T + b (N = 3E); returns (qkv, None, x)
+      cross attention:            q = LN(x) W[:E]^T + b[:E], kv = LN(x_kv) W[E:]^T + b[E:];
+                                  returns (q, kv, x)
+    The third output is x itself (a view) for the layer's residual: its gradient arrives here and
+    joins the LayerNorm backward in one kernel instead of an autograd add.  The weight gradient is
+    written per row block of the whole in_proj_weight (no slice scatter)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, w, b, eps):
+    def forward(ctx, x, x_kv, gamma, beta, w, b, eps):
         E = x.shape[-1]
         x2 = _rows_view(x, E).contiguous()
-        y, mean, rstd = rowgemm(x2, w, b, ln=(gamma, beta, eps), stats=True)
-        ctx.save_for_backward(x2, gamma, beta, w, mean, rstd)
-        ctx.eps, ctx.has_b, ctx.xshape = eps, b is not None, x.shape
-        return y.view(*x.shape[:-1], w.shape[0])
+        ln = (gamma, beta, eps)
+        if x_kv is None:
+            qkv, mean, rstd = rowgemm(x2, w, b, ln=ln, stats=True)
+            ctx.save_for_backward(x2, gamma, beta, w, mean, rstd)
+            q_out, kv_out = qkv, None
+        else:
+            k2 = _rows_view(x_kv, E).contiguous()
+            q_out, mean, rstd = rowgemm(x2, w[:E], b[:E] if b is not None else None, ln=ln, stats=True)
+            kv_out, mean_k, rstd_k = rowgemm(k2, w[E:], b[E:] if b is not None else None, ln=ln, stats=True)
+            ctx.save_for_backward(x2, gamma, beta, w, mean, rstd, k2, mean_k, rstd_k)
+        ctx.eps, ctx.has_b, ctx.xshape, ctx.kvshape = eps, b is not None, x.shape, (x_kv.shape if x_kv is not None
+                                                                                    else None)
+        return q_out, kv_out, x.view(x.shape)
 
     @staticmethod
-    def backward(ctx, dy):
-        x2, gamma, beta, w, mean, rstd = ctx.saved_tensors
-        N, K = w.shape
-        dy2 = _rows_view(dy, N).contiguous()
-        ln = (gamma, beta, ctx.eps)
-        dw, db = rowgemm_dw(x2, dy2, N, K, ctx.has_b, ln=ln, mean=mean, rstd=rstd)
-        dxn = rowgemm(dy2, w, transpose_w=True)
-        dx, dgamma, dbeta = row_layernorm_bwd(dxn, x2, gamma, mean, rstd)
-        return dx.view(ctx.xshape), dgamma, dbeta, dw, db, None
+    def backward(ctx, dq, dkv, dres):
+        E = ctx.xshape[-1]
+        ln_of = lambda g, b: (g, b, ctx.eps)  # noqa: E731
+        dres2 = _rows_view(dres, E).contiguous() if dres is not None else None
+        if ctx.kvshape is None:
+            x2, gamma, beta, w, mean, rstd = ctx.saved_tensors
+            dq2 = dq.contiguous()
+            dw, db = rowgemm_dw(x2, dq2, 3 * E, E, ctx.has_b, ln=ln_of(gamma, beta), mean=mean, rstd=rstd)
+            dxn = rowgemm(dq2, w, transpose_w=True)
+            dx, dgamma, dbeta = row_layernorm_bwd(dxn, x2, gamma, mean, rstd, dres2)
+            return dx.view(ctx.xshape), None, dgamma, dbeta, dw, db, None
+        x2, gamma, beta, w, mean, rstd, k2, mean_k, rstd_k = ctx.saved_tensors
+        dw = torch.empty_like(w)
+        db = torch.empty(3 * E, device=w.device, dtype=torch.float32) if ctx.has_b else None
+        ln = ln_of(gamma, beta)
+        dq2 = dq.contiguous()
+        rowgemm_dw(x2, dq2, E, E, ctx.has_b, ln=ln, mean=mean, rstd=rstd,
+                   out=(dw[:E], db[:E] if db is not None else None))
+        dxn = rowgemm(dq2, w[:E], transpose_w=True)
+        dx, dgamma, dbeta = row_layernorm_bwd(dxn, x2, gamma, mean, rstd, dres2)
+        dx_kv = None
+        if dkv is not None:
+            dkv2 = dkv.contiguous()
+            rowgemm_dw(k2, dkv2, 2 * E, E, ctx.has_b, ln=ln, mean=mean_k, rstd=rstd_k,
+                       out=(dw[E:], db[E:] if db is not None else None))
+            dxn_k = rowgemm(dkv2, w[E:], transpose_w=True)
+            dx_kv, dgk, dbk = row_layernorm_bwd(dxn_k, k2, gamma, mean_k, rstd_k)
+            dgamma, dbeta = dgamma + dgk, dbeta + dbk
+            dx_kv = dx_kv.view(ctx.kvshape)
+        else:
+            dw[E:].zero_()
+            if db is not None:
+                db[E:].zero_()
+        return dx.view(ctx.xshape), dx_kv, dgamma, dbeta, dw, db, None
 
 
 class _RowLinearResidual(torch.autograd.Function):
@@ -1211,21 +1255,13 @@ def encoder_layer_rows(x, x_kv, layer, diag, dropout_p, seed):
     value (the encoder passes the same embedded tensor for both), or None for self attention.
     Residual / ReLU dropouts must be inactive (the caller checks)."""
     attn = layer.self_attn
-    E = x.shape[-1]
     Tq, B = x.shape[0], x.shape[1]
     ln0, ln1 = layer.layer_norms[0], layer.layer_norms[1]
-    W, bW = attn.in_proj_weight, attn.in_proj_bias
-    if x_kv is None:
-        qkv = _RowLnLinear.apply(x, ln0.weight, ln0.bias, W, bW, float(ln0.eps)).view(-1, 3 * E)
-        q_src = kv_src = qkv
-        Tk = Tq
-    else:
-        q_src = _RowLnLinear.apply(x, ln0.weight, ln0.bias, W[:E], bW[:E] if bW is not None else None,
-                                   float(ln0.eps)).view(-1, E)
-        kv_src = _RowLnLinear.apply(x_kv, ln0.weight, ln0.bias, W[E:], bW[E:] if bW is not None else None,
-                                    float(ln0.eps)).view(-1, 2 * E)
-        Tk = x_kv.shape[0]
-    a = _MHARows.apply(q_src, kv_src, Tq, Tk, B, attn.num_heads_mult, diag, attn.scaling, dropout_p, seed)
-    x = _RowLinearResidual.apply(a, attn.out_proj.weight, attn.out_proj.bias, x)
+    q_src, kv_src, x_res = _RowLnQKV.apply(x, x_kv, ln0.weight, ln0.bias, attn.in_proj_weight, attn.in_proj_bias,
+                                           float(ln0.eps))
+    Tk = Tq if x_kv is None else x_kv.shape[0]
+    a = _MHARows.apply(q_src, kv_src if x_kv is not None else q_src, Tq, Tk, B, attn.num_heads_mult, diag,
+                       attn.scaling, dropout_p, seed)
+    x = _RowLinearResidual.apply(a, attn.out_proj.weight, attn.out_proj.bias, x_res)
     return _RowLnFfn.apply(x, ln1.weight, ln1.bias, layer.fc1.weight, layer.fc1.bias, layer.fc2.weight,
                            layer.fc2.bias, float(ln1.eps))
