@@ -54,28 +54,166 @@ struct RGArgs {
     float* rstd;
 };
 
-// 4 consecutive k (from k0) of row r of a (rows, ld) matrix; zeros past K / past the rows
+// Operand loads are branch-free and select-free: an element outside the tensor (row past the
+// end, k past K, n past N) is read from a 16-byte zero page instead, so every load is
+// unconditional and its value is first touched by the MFMA that consumes it.  (Loads under per-lane
+// branches got a full vmcnt(0) wait each, and a select right after a load pins the wait there too:
+// both serialised the DEPTH groups that are meant to be in flight.)
+__device__ __attribute__((aligned(16))) float g_zero4[4];
+
+// VEC: K, the leading dimension and the base are multiples of 4 floats (16-byte pieces).
+// 4 consecutive k (from k0) of row r (rok = the row exists); zeros past K
+template <bool VEC>
 __device__ __forceinline__ f4 load_k4(const float* base, int64_t r, int64_t ld, bool rok, int k0, int K) {
-    const float* p = base + r * ld + k0;
-    if (rok && k0 + 3 < K && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) return *reinterpret_cast<const f4*>(p);
-    f4 v = zero4();
+    if constexpr (VEC) {
+        // k0 and K are multiples of 4: k0 < K means all four are in
+        const float* p = (rok && k0 < K) ? base + r * ld + k0 : g_zero4;
+        return *reinterpret_cast<const f4*>(p);
+    } else {
+        f4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (rok && k0 + i < K) ? p[i] : 0.f;
-    return v;
+        for (int i = 0; i < 4; ++i) v[i] = *((rok && k0 + i < K) ? base + r * ld + k0 + i : g_zero4);
+        return v;
+    }
 }
 
-// W(n, k0 .. k0 + 3): k-contiguous (w_sk = 1) as a 16-byte piece, n-contiguous (the transpose) as
-// four scalars of rows k0 .. k0 + 3 (lanes of a group read 16 consecutive n: coalesced)
+// W(n, k0 .. k0 + 3): k-contiguous (an nn.Linear weight) as load_k4, or n-contiguous (TW, the
+// transpose for dX = dY W) as four scalars of rows k0 .. k0 + 3 (16 lanes of a group read 16
+// consecutive n: 64-byte pieces)
+template <bool VEC, bool TW>
 __device__ __forceinline__ f4 load_w4(const RGArgs& a, int n, int k0) {
     const bool nok = n < a.N;
-    if (a.w_sk == 1) return load_k4(a.w, n, a.w_sn, nok, k0, a.K);
-    f4 v = zero4();
+    if constexpr (!TW) {
+        return load_k4<VEC>(a.w, n, a.w_sn, nok, k0, a.K);
+    } else {
+        f4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (nok && k0 + i < a.K) ? a.w[(int64_t)(k0 + i) * a.w_sk + n] : 0.f;
-    return v;
+        for (int i = 0; i < 4; ++i)
+            v[i] = *((nok && k0 + i < a.K) ? a.w + (int64_t)(k0 + i) * a.w_sk + n : g_zero4);
+        return v;
+    }
 }
 
-template <bool LN>
+struct Tile {
+    f4 acc[2][2];   // [m tile][n tile], D[row 4 g + i][col t]
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+    }
+    // one group: 4 k-steps x (2 x 2) tiles, four independent accumulator chains
+    __device__ __forceinline__ void group(f4 xa, f4 xb, f4 wa, f4 wb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc[0][0] = mfma(xa[i], wa[i], acc[0][0]);
+            acc[0][1] = mfma(xa[i], wb[i], acc[0][1]);
+            acc[1][0] = mfma(xb[i], wa[i], acc[1][0]);
+            acc[1][1] = mfma(xb[i], wb[i], acc[1][1]);
+        }
+    }
+};
+
+// Plain rows: X and W stream through a DEPTH-slot register ring.  Whole laps of DEPTH groups run
+// in a loop with no exits (a slot is refilled right after its MFMAs, so the ring keeps its
+// registers and the wait before each group leaves the other DEPTH - 1 groups in flight), the
+// NG % DEPTH tail after it.
+template <bool VEC, bool TW>
+__device__ __forceinline__ void stream_rows(const RGArgs& a, Tile& T, int64_t ra, int64_t rb, bool oka, bool okb,
+                                            int na, int nb, int g, int NG) {
+    f4 xa[DEPTH], xb[DEPTH], wa[DEPTH], wb[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        const int k0 = KG * d + 4 * g;   // groups past K load as zeros
+        xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
+        xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
+        wa[d] = load_w4<VEC, TW>(a, na, k0);
+        wb[d] = load_w4<VEC, TW>(a, nb, k0);
+    }
+    const int laps = NG / DEPTH;
+    for (int l = 0; l < laps; ++l) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            T.group(xa[d], xb[d], wa[d], wb[d]);
+            const int k0 = KG * ((l + 1) * DEPTH + d) + 4 * g;
+            xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
+            xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
+            wa[d] = load_w4<VEC, TW>(a, na, k0);
+            wb[d] = load_w4<VEC, TW>(a, nb, k0);
+        }
+    }
+    const int rem = NG - laps * DEPTH;
+#pragma unroll
+    for (int d = 0; d < DEPTH - 1; ++d)
+        if (d < rem) T.group(xa[d], xb[d], wa[d], wb[d]);
+}
+
+// LayerNorm rows (K <= KMAX_LN): the two rows' whole K extent in registers (NG groups, a template
+// constant so every index is static and nothing branches), statistics by the 4 lane groups, and
+// W, gamma, beta streaming through the ring; the W / gamma / beta prologue is issued before the
+// statistics so it lands while they are computed.
+template <bool VEC, int NG>
+__device__ __forceinline__ void ln_rows(const RGArgs& a, Tile& T, int64_t ra, int64_t rb, bool oka, bool okb,
+                                        int na, int nb, int g, bool write_stats) {
+    f4 xa[NG], xb[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        xa[j] = load_k4<VEC>(a.x, ra, a.ldx, oka, KG * j + 4 * g, a.K);
+        xb[j] = load_k4<VEC>(a.x, rb, a.ldx, okb, KG * j + 4 * g, a.K);
+    }
+    constexpr int D = NG < DEPTH ? NG : DEPTH;
+    f4 wa[D], wb[D], ga[D], be[D];
+    auto refill = [&](int slot, int j) {
+        const int k0 = KG * j + 4 * g;   // zeros past K
+        wa[slot] = load_w4<VEC, false>(a, na, k0);
+        wb[slot] = load_w4<VEC, false>(a, nb, k0);
+        ga[slot] = load_k4<VEC>(a.gamma, 0, 0, true, k0, a.K);
+        be[slot] = load_k4<VEC>(a.beta, 0, 0, true, k0, a.K);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) refill(d, d);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        sa += (xa[j][0] + xa[j][1]) + (xa[j][2] + xa[j][3]);
+        sb += (xb[j][0] + xb[j][1]) + (xb[j][2] + xb[j][3]);
+    }
+    sa += __shfl_xor(sa, 16); sa += __shfl_xor(sa, 32);
+    sb += __shfl_xor(sb, 16); sb += __shfl_xor(sb, 32);
+    const float invK = 1.0f / (float)a.K;
+    const float ma = sa * invK, mb = sb * invK;
+    float va = 0.f, vb = 0.f;
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = KG * j + 4 * g + i < a.K;
+            const float da = in ? xa[j][i] - ma : 0.f, db = in ? xb[j][i] - mb : 0.f;
+            va = fmaf(da, da, va);
+            vb = fmaf(db, db, vb);
+        }
+    va += __shfl_xor(va, 16); va += __shfl_xor(va, 32);
+    vb += __shfl_xor(vb, 16); vb += __shfl_xor(vb, 32);
+    const float rsa = 1.0f / sqrtf(va * invK + a.eps), rsb = 1.0f / sqrtf(vb * invK + a.eps);
+    if (write_stats && g == 0) {
+        if (oka) { a.mean[ra] = ma; a.rstd[ra] = rsa; }
+        if (okb) { a.mean[rb] = mb; a.rstd[rb] = rsb; }
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int s = j % D;
+        f4 xna, xnb;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xna[i] = fmaf((xa[j][i] - ma) * rsa, ga[s][i], be[s][i]);
+            xnb[i] = fmaf((xb[j][i] - mb) * rsb, ga[s][i], be[s][i]);
+        }
+        T.group(xna, xnb, wa[s], wb[s]);
+        if (j + D < NG) refill(s, j + D);   // compile-time condition
+    }
+}
+
+template <bool LN, bool VEC, bool TW>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t = lane & 15, g = lane >> 4;
@@ -84,133 +222,58 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
     const int64_t ra = m0 + t, rb = m0 + 16 + t;                       // A rows of the two m tiles
     const bool oka = ra < a.rows, okb = rb < a.rows;
     const int na = n0 + t, nb = n0 + 16 + t;                           // B columns of the two n tiles
+    if (m0 >= a.rows || n0 >= a.N) return;   // a wave wholly past the edge (no barriers here)
     const int NG = (a.K + KG - 1) / KG;
-    f4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
-    auto mma_group = [&](f4 xa, f4 xb, f4 wa, f4 wb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            acc[0][0] = mfma(xa[i], wa[i], acc[0][0]);
-            acc[0][1] = mfma(xa[i], wb[i], acc[0][1]);
-            acc[1][0] = mfma(xb[i], wa[i], acc[1][0]);
-            acc[1][1] = mfma(xb[i], wb[i], acc[1][1]);
-        }
-    };
+    Tile T;
+    T.zero();
     if constexpr (LN) {
-        // the two rows' whole K extent in registers, LayerNorm statistics by the 4 lane groups
-        constexpr int MG = KMAX_LN / KG;
-        f4 xa[MG], xb[MG];
-#pragma unroll
-        for (int j = 0; j < MG; ++j) {
-            if (j < NG) {
-                xa[j] = load_k4(a.x, ra, a.ldx, oka, KG * j + 4 * g, a.K);
-                xb[j] = load_k4(a.x, rb, a.ldx, okb, KG * j + 4 * g, a.K);
-            } else {
-                xa[j] = xb[j] = zero4();
-            }
-        }
-        float sa = 0.f, sb = 0.f;
-#pragma unroll
-        for (int j = 0; j < MG; ++j) {
-            sa += (xa[j][0] + xa[j][1]) + (xa[j][2] + xa[j][3]);
-            sb += (xb[j][0] + xb[j][1]) + (xb[j][2] + xb[j][3]);
-        }
-        sa += __shfl_xor(sa, 16); sa += __shfl_xor(sa, 32);
-        sb += __shfl_xor(sb, 16); sb += __shfl_xor(sb, 32);
-        const float invK = 1.0f / (float)a.K;
-        const float ma = sa * invK, mb = sb * invK;
-        float va = 0.f, vb = 0.f;
-#pragma unroll
-        for (int j = 0; j < MG; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const bool in = KG * j + 4 * g + i < a.K;
-                const float da = in ? xa[j][i] - ma : 0.f, db = in ? xb[j][i] - mb : 0.f;
-                va = fmaf(da, da, va);
-                vb = fmaf(db, db, vb);
-            }
-        va += __shfl_xor(va, 16); va += __shfl_xor(va, 32);
-        vb += __shfl_xor(vb, 16); vb += __shfl_xor(vb, 32);
-        const float rsa = 1.0f / sqrtf(va * invK + a.eps), rsb = 1.0f / sqrtf(vb * invK + a.eps);
-        if (a.mean != nullptr && blockIdx.y == 0 && (wave >> 1) == 0 && g == 0) {
-            if (oka) { a.mean[ra] = ma; a.rstd[ra] = rsa; }
-            if (okb) { a.mean[rb] = mb; a.rstd[rb] = rsb; }
-        }
-        f4 wa[DEPTH], wb[DEPTH];
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-            wa[d] = d < NG ? load_w4(a, na, KG * d + 4 * g) : zero4();
-            wb[d] = d < NG ? load_w4(a, nb, KG * d + 4 * g) : zero4();
-        }
-#pragma unroll
-        for (int j = 0; j < MG; ++j) {
-            if (j < NG) {
-            f4 ga, gb, xna, xnb;
-            const int k0 = KG * j + 4 * g;
-            ga = load_k4(a.gamma, 0, 0, true, k0, a.K);
-            gb = load_k4(a.beta, 0, 0, true, k0, a.K);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                xna[i] = fmaf((xa[j][i] - ma) * rsa, ga[i], gb[i]);
-                xnb[i] = fmaf((xb[j][i] - mb) * rsb, ga[i], gb[i]);
-            }
-            const f4 wcur_a = wa[j % DEPTH], wcur_b = wb[j % DEPTH];
-            if (j + DEPTH < NG) {
-                wa[j % DEPTH] = load_w4(a, na, KG * (j + DEPTH) + 4 * g);
-                wb[j % DEPTH] = load_w4(a, nb, KG * (j + DEPTH) + 4 * g);
-            }
-            mma_group(xna, xnb, wcur_a, wcur_b);
-            }
+        const bool ws = a.mean != nullptr && blockIdx.y == 0 && (wave >> 1) == 0;
+        switch (NG) {
+#define MMNI_LN_CASE(n) case n: ln_rows<VEC, n>(a, T, ra, rb, oka, okb, na, nb, g, ws); break;
+            MMNI_LN_CASE(1) MMNI_LN_CASE(2) MMNI_LN_CASE(3) MMNI_LN_CASE(4) MMNI_LN_CASE(5) MMNI_LN_CASE(6)
+            MMNI_LN_CASE(7) MMNI_LN_CASE(8) MMNI_LN_CASE(9) MMNI_LN_CASE(10) MMNI_LN_CASE(11)
+#undef MMNI_LN_CASE
+            default: break;   // K > KMAX_LN is refused by the host
         }
     } else {
-        // stream K in groups, DEPTH groups of all four operands in flight
-        f4 xa[DEPTH], xb[DEPTH], wa[DEPTH], wb[DEPTH];
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-            const int k0 = KG * d + 4 * g;
-            const bool v = d < NG;
-            xa[d] = v ? load_k4(a.x, ra, a.ldx, oka, k0, a.K) : zero4();
-            xb[d] = v ? load_k4(a.x, rb, a.ldx, okb, k0, a.K) : zero4();
-            wa[d] = v ? load_w4(a, na, k0) : zero4();
-            wb[d] = v ? load_w4(a, nb, k0) : zero4();
-        }
-        for (int j0 = 0; j0 < NG; j0 += DEPTH) {
-#pragma unroll
-            for (int d = 0; d < DEPTH; ++d) {
-                const int j = j0 + d;
-                if (j >= NG) break;
-                const f4 ca = xa[d], cb = xb[d], cwa = wa[d], cwb = wb[d];
-                if (j + DEPTH < NG) {
-                    const int k0 = KG * (j + DEPTH) + 4 * g;
-                    xa[d] = load_k4(a.x, ra, a.ldx, oka, k0, a.K);
-                    xb[d] = load_k4(a.x, rb, a.ldx, okb, k0, a.K);
-                    wa[d] = load_w4(a, na, k0);
-                    wb[d] = load_w4(a, nb, k0);
-                }
-                mma_group(ca, cb, cwa, cwb);
-            }
-        }
+        stream_rows<VEC, TW>(a, T, ra, rb, oka, okb, na, nb, g, NG);
     }
-    // epilogue: D[row 4 g + i][col t] of tile (mi, ni)
+    auto& acc = T.acc;
+    // epilogue: D[row 4 g + i][col t] of tile (mi, ni).  The residual / ReLU-mask operands load
+    // unconditionally first (absent ones read y's first row, clamped addresses; the host passes
+    // ld 0) and are selected, so the stores wait once, not per element.
+    const bool has_aux = a.aux != nullptr, has_res = a.res != nullptr;
+    const float* auxp = has_aux ? a.aux : a.y;
+    const float* resp = has_res ? a.res : a.y;
+    float ev[2][2][4], rv[2][2][4];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
         const int n = n0 + 16 * ni + t;
-        if (n >= a.N) continue;
-        const float b = a.bias ? a.bias[n] : 0.f;
+        const int nc = n < a.N ? n : a.N - 1;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t r = m0 + 16 * mi + 4 * g + i;
+                const int64_t rc = r < a.rows ? r : a.rows - 1;
+                ev[ni][mi][i] = auxp[rc * a.ldaux + nc];
+                rv[ni][mi][i] = resp[rc * a.ldres + nc];
+            }
+    }
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+        const int n = n0 + 16 * ni + t;
+        const float b = a.bias ? a.bias[n < a.N ? n : a.N - 1] : 0.f;
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int64_t r = m0 + 16 * mi + 4 * g + i;
-                if (r >= a.rows) continue;
                 float v = acc[mi][ni][i] + b;
                 if (a.relu) v = fmaxf(v, 0.f);
-                if (a.aux != nullptr && !(a.aux[r * a.ldaux + n] > 0.f)) v = 0.f;
-                if (a.res != nullptr) v += a.res[r * a.ldres + n];
-                a.y[r * a.ldy + n] = v;
+                if (has_aux && !(ev[ni][mi][i] > 0.f)) v = 0.f;
+                if (has_res) v += rv[ni][mi][i];
+                if (r < a.rows && n < a.N) a.y[r * a.ldy + n] = v;
             }
         }
     }
@@ -232,76 +295,90 @@ struct DWArgs {
     float* part;   // [chunk][N * K + N]: dW row-major, then db
 };
 
-// rows r0 + 16 j + 4 g + i (i = 0..3) of column c (scalars; the 16 lanes of a group read 16
-// consecutive columns of each row)
+// rows r0 .. r0 + 3 of column c (scalars; the 16 lanes of a group read 16 consecutive columns of
+// each row); the zero page past the chunk end / past C
 __device__ __forceinline__ f4 load_rows4(const float* base, int64_t ld, int64_t r0, int64_t rend, int c, int C) {
-    f4 v = zero4();
+    f4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (r0 + i < rend && c < C) ? base[(r0 + i) * ld + c] : 0.f;
+    for (int i = 0; i < 4; ++i) v[i] = *((r0 + i < rend && c < C) ? base + (r0 + i) * ld + c : g_zero4);
     return v;
 }
 
+// the row statistics of rows r0 .. r0 + 3 (zero page past the chunk: those rows are masked later)
+__device__ __forceinline__ f4 load_stat4(const float* p, int64_t r0, int64_t rend) {
+    f4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = *(r0 + i < rend ? p + r0 + i : g_zero4);
+    return v;
+}
+
+template <bool LN>
 __global__ __launch_bounds__(256) void rowgemm_dw_kernel(DWArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t = lane & 15, g = lane >> 4;
     const int n0 = blockIdx.x * BN + (wave & 1) * 32, k0 = blockIdx.y * BN + (wave >> 1) * 32;
     const int64_t rbeg = (int64_t)blockIdx.z * a.rows_per_chunk;
     const int64_t rend = rbeg + a.rows_per_chunk < a.rows ? rbeg + a.rows_per_chunk : a.rows;
+    if (n0 >= a.N || k0 > a.K) return;   // a wave wholly past the edge (its partials are never read)
     const int na = n0 + t, nb = n0 + 16 + t, ka = k0 + t, kb = k0 + 16 + t;
+    // X' columns ka, kb: LN affine per column (hoisted), the ones column k == K (db), zeros past it
+    const float ga = LN ? a.gamma[ka < a.K ? ka : a.K - 1] : 1.f, ba = LN ? a.beta[ka < a.K ? ka : a.K - 1] : 0.f;
+    const float gb = LN ? a.gamma[kb < a.K ? kb : a.K - 1] : 1.f, bb = LN ? a.beta[kb < a.K ? kb : a.K - 1] : 0.f;
     f4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
-    // X' column k of rows r..r+3: LayerNorm recompute, the ones column k == K (db), zeros past it
-    auto load_x = [&](int64_t r, int k) {
-        f4 v = zero4();
+    // raw X -> X' at the consuming step (k >= K reads the zero page; the ones column set here)
+    auto xform = [&](f4 xv, f4 m, f4 rs, int64_t r, int k, float gk, float bk) {
+        f4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int64_t rr = r + i;
-            if (rr < rend && k < a.K) {
-                float xv = a.x[rr * a.ldx + k];
-                if (a.ln) xv = fmaf((xv - a.mean[rr]) * a.rstd[rr], a.gamma[k], a.beta[k]);
-                v[i] = xv;
-            } else if (rr < rend && k == a.K) {
-                v[i] = 1.0f;
-            }
+            float xn = LN ? fmaf((xv[i] - m[i]) * rs[i], gk, bk) : xv[i];
+            xn = k < a.K ? xn : (k == a.K ? 1.f : 0.f);
+            v[i] = r + i < rend ? xn : 0.f;
         }
         return v;
     };
     const int NG = (int)((rend - rbeg + KG - 1) / KG);
-    f4 da[DEPTH], db[DEPTH], xa[DEPTH], xb[DEPTH];
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-        const int64_t r = rbeg + KG * d + 4 * g;
+    f4 da[DEPTH], db[DEPTH], xa[DEPTH], xb[DEPTH], mr[DEPTH], rr[DEPTH];
+    auto issue = [&](int d, int64_t r) {
         da[d] = load_rows4(a.dy, a.lddy, r, rend, na, a.N);
         db[d] = load_rows4(a.dy, a.lddy, r, rend, nb, a.N);
-        xa[d] = load_x(r, ka);
-        xb[d] = load_x(r, kb);
-    }
-    for (int j0 = 0; j0 < NG; j0 += DEPTH) {
+        xa[d] = load_rows4(a.x, a.ldx, r, rend, ka, a.K);
+        xb[d] = load_rows4(a.x, a.ldx, r, rend, kb, a.K);
+        if (LN) {
+            mr[d] = load_stat4(a.mean, r, rend);
+            rr[d] = load_stat4(a.rstd, r, rend);
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) issue(d, rbeg + KG * d + 4 * g);   // rows past the chunk: zeros
+    // A[row n][kk = row]: dY;  B[kk = row][col k]: X'.  Whole laps in an exit-free loop, slots
+    // refilled after their MFMAs (as stream_rows), then the tail.
+    auto step = [&](int d, int j) {
+        const int64_t r = rbeg + KG * j + 4 * g;
+        const f4 cxa = xform(xa[d], mr[d], rr[d], r, ka, ga, ba), cxb = xform(xb[d], mr[d], rr[d], r, kb, gb, bb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc[0][0] = mfma(da[d][i], cxa[i], acc[0][0]);
+            acc[0][1] = mfma(da[d][i], cxb[i], acc[0][1]);
+            acc[1][0] = mfma(db[d][i], cxa[i], acc[1][0]);
+            acc[1][1] = mfma(db[d][i], cxb[i], acc[1][1]);
+        }
+    };
+    const int laps = NG / DEPTH;
+    for (int l = 0; l < laps; ++l) {
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
-            const int j = j0 + d;
-            if (j >= NG) break;
-            const f4 ca = da[d], cb = db[d], cxa = xa[d], cxb = xb[d];
-            if (j + DEPTH < NG) {
-                const int64_t r = rbeg + KG * (j + DEPTH) + 4 * g;
-                da[d] = load_rows4(a.dy, a.lddy, r, rend, na, a.N);
-                db[d] = load_rows4(a.dy, a.lddy, r, rend, nb, a.N);
-                xa[d] = load_x(r, ka);
-                xb[d] = load_x(r, kb);
-            }
-            // A[row n][kk = row]: dY;  B[kk = row][col k]: X'
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                acc[0][0] = mfma(ca[i], cxa[i], acc[0][0]);
-                acc[0][1] = mfma(ca[i], cxb[i], acc[0][1]);
-                acc[1][0] = mfma(cb[i], cxa[i], acc[1][0]);
-                acc[1][1] = mfma(cb[i], cxb[i], acc[1][1]);
-            }
+            step(d, l * DEPTH + d);
+            issue(d, rbeg + KG * ((l + 1) * DEPTH + d) + 4 * g);
         }
     }
+    const int rem = NG - laps * DEPTH;
+#pragma unroll
+    for (int d = 0; d < DEPTH - 1; ++d)
+        if (d < rem) step(d, laps * DEPTH + d);
     // D[row n = 4 g + i][col k = t]
     float* p = a.part + (int64_t)blockIdx.z * ((int64_t)a.N * a.K + a.N);
 #pragma unroll
@@ -319,36 +396,52 @@ __global__ __launch_bounds__(256) void rowgemm_dw_kernel(DWArgs a) {
         }
 }
 
-// out[j] = sum_c part[c][j] in chunk order (deterministic); columns [0, split) -> out, [split, ncols)
-// -> out2 (nullable).  One thread per 4 columns, every chunk's load issued before the adds.
+// out[j] = sum_c part[c][j] (deterministic: fixed slices and a fixed tree); columns [0, split) ->
+// out, [split, ncols) -> out2 (nullable).  A block owns 32 columns (8 float4 quads) and splits the
+// chunks over 32 slices (slice s sums chunks s, s + 32, ... in order, 8 loads in flight), then adds
+// the slices by a fixed LDS tree.  One thread per column quad looping over 100+ chunks was a chain
+// of dependent load waits (~10 us per call).
+constexpr int kCsSlices = 32, kCsQuads = 8;
 __global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ part, int nchunks, int ncols,
                                                         int split, float* out, float* out2) {
-    const int j4 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (j4 >= ncols) return;
+    __shared__ f4 red[kCsSlices][kCsQuads];
+    const int q = threadIdx.x % kCsQuads, sl = threadIdx.x / kCsQuads;
+    const int j4 = (blockIdx.x * kCsQuads + q) * 4;
+    const bool vec = (ncols & 3) == 0;
     f4 s = zero4();
-    const bool vec = j4 + 3 < ncols && (ncols & 3) == 0;
-    for (int c0 = 0; c0 < nchunks; c0 += 8) {
+    for (int c0 = sl; c0 < nchunks; c0 += 8 * kCsSlices) {
         f4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            v[u] = zero4();
-            if (c0 + u < nchunks) {
-                const float* p = part + (int64_t)(c0 + u) * ncols + j4;
-                if (vec) v[u] = *reinterpret_cast<const f4*>(p);
-                else
+            const int c = c0 + u * kCsSlices;
+            const float* p = part + (int64_t)(c < nchunks ? c : nchunks - 1) * ncols;
+            if (vec) {
+                v[u] = *reinterpret_cast<const f4*>(p + (j4 < ncols ? j4 : ncols - 4));
+            } else {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) v[u][i] = j4 + i < ncols ? p[i] : 0.f;
+                for (int i = 0; i < 4; ++i) v[u][i] = p[j4 + i < ncols ? j4 + i : ncols - 1];
             }
+            if (c >= nchunks) v[u] = zero4();
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) s += v[u];
     }
+    red[sl][q] = s;
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int j = j4 + i;
-        if (j >= ncols) break;
-        if (j < split) out[j] = s[i];
-        else if (out2 != nullptr) out2[j - split] = s[i];
+    for (int h = kCsSlices / 2; h > 0; h >>= 1) {
+        if (sl < h) red[sl][q] += red[sl + h][q];
+        __syncthreads();
+    }
+    if (sl == 0) {
+        const f4 r = red[0][q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = j4 + i;
+            if (j >= ncols) break;
+            if (j < split) out[j] = r[i];
+            else if (out2 != nullptr) out2[j - split] = r[i];
+        }
     }
 }
 
@@ -368,24 +461,33 @@ struct LNBArgs {
     float* part;   // [block][2C]: dgamma | dbeta
 };
 
+template <bool RES>
 __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
     __shared__ float red[4][2][256];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f}, gm[4];
+    int cc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = lane + 64 * j;
-        gm[j] = c < a.C ? a.gamma[c] : 0.f;
+        cc[j] = c < a.C ? c : a.C - 1;   // clamped column: every load unconditional
+        gm[j] = c < a.C ? a.gamma[cc[j]] : 0.f;
     }
     const float invC = 1.0f / (float)a.C;
     for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.rows; r += (int64_t)gridDim.x * 4) {
         const float m = a.mean[r], rs = a.rstd[r];
-        float d[4], xh[4], s1 = 0.f, s2 = 0.f;
+        float d[4], xv[4], rv[4], xh[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int c = lane + 64 * j;
-            d[j] = c < a.C ? a.dxn[r * a.lddxn + c] : 0.f;
-            xh[j] = c < a.C ? (a.x[r * a.ldx + c] - m) * rs : 0.f;
+            d[j] = a.dxn[r * a.lddxn + cc[j]];
+            xv[j] = a.x[r * a.ldx + cc[j]];
+            rv[j] = RES ? a.dres[r * a.ldres + cc[j]] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool in = lane + 64 * j < a.C;
+            d[j] = in ? d[j] : 0.f;
+            xh[j] = in ? (xv[j] - m) * rs : 0.f;
             const float gd = d[j] * gm[j];
             s1 += gd;
             s2 = fmaf(gd, xh[j], s2);
@@ -401,10 +503,8 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = lane + 64 * j;
-            if (c >= a.C) continue;
-            float v = rs * (d[j] * gm[j] - s1 - xh[j] * s2);
-            if (a.dres != nullptr) v += a.dres[r * a.ldres + c];
-            a.dx[r * a.lddx + c] = v;
+            const float v = rs * (d[j] * gm[j] - s1 - xh[j] * s2) + rv[j];
+            if (c < a.C) a.dx[r * a.lddx + c] = v;
         }
     }
 #pragma unroll
@@ -420,7 +520,7 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
     }
 }
 
-constexpr int kLnbBlocks = 128;
+constexpr int kLnbBlocks = 768;   // ~2 rows per wave at 6,912 rows: a short dependent chain per wave
 
 // row chunks of a weight gradient: >= 64 rows each (4 groups per wave), at most 256, and a
 // partial slab of at most 8 MB (the chunk-order reduction reads it once)
@@ -434,8 +534,9 @@ int dw_chunks(int64_t rows, int N, int K) {
 }
 
 void chunk_sum(const float* part, int nchunks, int ncols, int split, float* out, float* out2, hipStream_t s) {
-    const int threads = (ncols + 3) / 4;
-    chunk_sum_kernel<<<(threads + 255) / 256, 256, 0, s>>>(part, nchunks, ncols, split, out, out2);
+    const int cols_per_block = 4 * kCsQuads;
+    chunk_sum_kernel<<<(ncols + cols_per_block - 1) / cols_per_block, 256, 0, s>>>(part, nchunks, ncols, split, out,
+                                                                                  out2);
 }
 
 }  // namespace enc
@@ -463,9 +564,25 @@ extern "C" int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const fl
     a.w_sn = d->w_sn; a.w_sk = d->w_sk; a.K = d->K; a.N = d->N; a.ln = d->ln; a.relu = d->relu; a.eps = d->eps;
     a.x = x; a.gamma = gamma; a.beta = beta; a.w = w; a.bias = bias; a.aux = aux; a.res = res; a.y = y;
     a.mean = d->ln ? mean : nullptr; a.rstd = d->ln ? rstd : nullptr;
+    if (aux == nullptr) a.ldaux = 0;
+    if (res == nullptr) a.ldres = 0;
+    const bool tw = d->w_sk != 1;
+    const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    // 16-byte operand pieces when every row of x (and of a k-contiguous weight) starts aligned
+    const bool vec = d->K % 4 == 0 && d->ldx % 4 == 0 && al(x) && (!d->ln || (al(gamma) && al(beta))) &&
+                     (tw || (d->w_sn % 4 == 0 && al(w)));
     const dim3 grid((unsigned)((d->rows + enc::BM - 1) / enc::BM), (unsigned)((d->N + enc::BN - 1) / enc::BN));
-    if (d->ln) enc::rowgemm_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-    else enc::rowgemm_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    hipStream_t s = (hipStream_t)stream;
+#define MMNI_RG(LN, VEC, TW) enc::rowgemm_kernel<LN, VEC, TW><<<grid, 256, 0, s>>>(a)
+    if (d->ln) {
+        MMNI_ARG_CHECK(!tw, "rowgemm: the LayerNorm prologue takes a k-contiguous weight");
+        if (vec) MMNI_RG(true, true, false); else MMNI_RG(true, false, false);
+    } else if (tw) {
+        if (vec) MMNI_RG(false, true, true); else MMNI_RG(false, false, true);
+    } else {
+        if (vec) MMNI_RG(false, true, false); else MMNI_RG(false, false, false);
+    }
+#undef MMNI_RG
     return launch_status("rowgemm");
 }
 
@@ -489,7 +606,8 @@ extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const
     a.part = static_cast<float*>(workspace);
     const dim3 grid((unsigned)((d->N + enc::BN - 1) / enc::BN), (unsigned)((d->K + 1 + enc::BN - 1) / enc::BN),
                     (unsigned)chunks);
-    enc::rowgemm_dw_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    if (d->ln) enc::rowgemm_dw_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else enc::rowgemm_dw_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     int rc = launch_status("rowgemm_dw");
     if (rc) return rc;
     // dW = columns [0, N K), db = [N K, N K + N) (a null db drops them)
@@ -517,7 +635,8 @@ extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int
     a.part = static_cast<float*>(workspace);
     int64_t blocks = (rows + 3) / 4;
     if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
-    enc::row_ln_bwd_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
+    if (dres != nullptr) enc::row_ln_bwd_kernel<true><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
+    else enc::row_ln_bwd_kernel<false><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
     int rc = launch_status("row_layernorm_bwd");
     if (rc) return rc;
     enc::chunk_sum(a.part, (int)blocks, 2 * C, C, dgamma, dbeta, (hipStream_t)stream);

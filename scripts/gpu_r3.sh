@@ -33,6 +33,11 @@ if has ab && [ -f build/base.so ]; then
     done
   done
 fi
+if has encb; then
+  timeout -k 10 300 python3 scripts/bench_encoder.py 20 > gpurun_out/encb_$TAG.json 2> gpurun_out/encb_$TAG.err
+  rc=$?; echo "encoder bench rc=$rc"; cut -c1-150 gpurun_out/encb_$TAG.json; tail -2 gpurun_out/encb_$TAG.err
+  fatal $rc && exit $rc
+fi
 if has bench; then
   timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
   rc=$?; echo "bench rc=$rc"; python3 -c "
@@ -55,6 +60,20 @@ import json; d=json.loads(open('gpurun_out/bench_c5_$TAG.json').read().strip().s
 print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_ms'])" ; tail -2 gpurun_out/bench_c5_$TAG.err
   fatal $rc && exit $rc
 fi
+for c in c2; do
+  if has bench$c; then
+    timeout -k 10 600 python bench.py --config $c --steps 20 --warmup 5 > gpurun_out/bench_${c}_$TAG.json 2> gpurun_out/bench_${c}_$TAG.err
+    rc=$?; echo "bench $c rc=$rc"; tail -1 gpurun_out/bench_${c}_$TAG.json | cut -c1-600; tail -2 gpurun_out/bench_${c}_$TAG.err
+    fatal $rc && exit $rc
+  fi
+  if has prof$c; then
+    R="$GRAFT_REPO_ROOT"
+    ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof_${c}_$TAG" -o k -- \
+        python3 "$R/bench.py" --config $c --no-cpu-baseline --steps 20 --warmup 5 > "$R/gpurun_out/prof_${c}_$TAG.json" 2> "$R/gpurun_out/prof_${c}_$TAG.err" )
+    rc=$?; echo "prof $c rc=$rc"; fatal $rc && exit $rc
+    f=$(find gpurun_out/prof_${c}_$TAG -name "*kernel_stats.csv" | head -1); head -25 "$f" | cut -c1-200
+  fi
+done
 if has profc4; then
   R="$GRAFT_REPO_ROOT"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof_c4_$TAG" -o k -- \
