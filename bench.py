@@ -344,7 +344,9 @@ def main():
         if live:
             raise SystemExit(f"bench.py: hipGraph capture with attention dropout in training ({live[0]}, ...) "
                              "would freeze the dropout mask; run with --eager")
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph)
+    # fused: one multi-tensor launch per step (the foreach path issued ~300 one-block divides per
+    # step at C2 — per-tensor fallbacks of its capturable bias corrections)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=graph, fused=True)
     A, B, y = synthetic_pairs(args.batch, args.size, device, seed=1234 + rank,
                               size_b=args.size * 3 // 4 if args.config == "c5" else None)
     inputs = (A,) if args.config == "c2" else (A, B)

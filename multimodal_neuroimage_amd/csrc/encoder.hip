@@ -36,7 +36,9 @@ __device__ __forceinline__ f4 zero4() { return (f4){0.f, 0.f, 0.f, 0.f}; }
 constexpr int BM = 64, BN = 64;
 constexpr int KG = 16;       // k per group (4 k-steps)
 constexpr int KMAX_LN = 176; // LN prologue: the whole row (K <= 176, 11 groups) held in registers
-constexpr int DEPTH = 4;     // groups in flight
+constexpr int DEPTH = 4;     // groups in flight (LN rows, weight gradient)
+constexpr int SDEPTH = 8;    // groups in flight for plain rows: 7 groups (~3.5k cycles of MFMA) cover a
+                             // first-touch HBM latency at ~1 wave per SIMD
 
 struct RGArgs {
     int64_t rows, ldx, ldy, ldres, ldaux, w_sn, w_sk;
@@ -114,37 +116,37 @@ struct Tile {
     }
 };
 
-// Plain rows: X and W stream through a DEPTH-slot register ring.  Whole laps of DEPTH groups run
+// Plain rows: X and W stream through an SDEPTH-slot register ring.  Whole laps of SDEPTH groups run
 // in a loop with no exits (a slot is refilled right after its MFMAs, so the ring keeps its
-// registers and the wait before each group leaves the other DEPTH - 1 groups in flight), the
-// NG % DEPTH tail after it.
+// registers and the wait before each group leaves the other SDEPTH - 1 groups in flight), the
+// NG % SDEPTH tail after it.
 template <bool VEC, bool TW>
 __device__ __forceinline__ void stream_rows(const RGArgs& a, Tile& T, int64_t ra, int64_t rb, bool oka, bool okb,
                                             int na, int nb, int g, int NG) {
-    f4 xa[DEPTH], xb[DEPTH], wa[DEPTH], wb[DEPTH];
+    f4 xa[SDEPTH], xb[SDEPTH], wa[SDEPTH], wb[SDEPTH];
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
+    for (int d = 0; d < SDEPTH; ++d) {
         const int k0 = KG * d + 4 * g;   // groups past K load as zeros
         xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
         xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
         wa[d] = load_w4<VEC, TW>(a, na, k0);
         wb[d] = load_w4<VEC, TW>(a, nb, k0);
     }
-    const int laps = NG / DEPTH;
+    const int laps = NG / SDEPTH;
     for (int l = 0; l < laps; ++l) {
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
+        for (int d = 0; d < SDEPTH; ++d) {
             T.group(xa[d], xb[d], wa[d], wb[d]);
-            const int k0 = KG * ((l + 1) * DEPTH + d) + 4 * g;
+            const int k0 = KG * ((l + 1) * SDEPTH + d) + 4 * g;
             xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
             xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
             wa[d] = load_w4<VEC, TW>(a, na, k0);
             wb[d] = load_w4<VEC, TW>(a, nb, k0);
         }
     }
-    const int rem = NG - laps * DEPTH;
+    const int rem = NG - laps * SDEPTH;
 #pragma unroll
-    for (int d = 0; d < DEPTH - 1; ++d)
+    for (int d = 0; d < SDEPTH - 1; ++d)
         if (d < rem) T.group(xa[d], xb[d], wa[d], wb[d]);
 }
 
@@ -586,9 +588,60 @@ extern "C" int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const fl
     return launch_status("rowgemm");
 }
 
+namespace mmni {
+
+size_t enc_rowgemm_dw_workspace(int64_t rows, int N, int K) {
+    return (size_t)enc::dw_chunks(rows, N, K) * ((size_t)N * K + N) * sizeof(float);
+}
+
+int enc_rowgemm_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy, int64_t lddy,
+                   const float* gamma, const float* beta, const float* mean, const float* rstd, float* dw, float* db,
+                   void* workspace, hipStream_t s) {
+    enc::DWArgs a{};
+    a.rows = rows; a.ldx = ldx; a.lddy = lddy; a.K = K; a.N = N; a.ln = gamma != nullptr;
+    const int chunks = enc::dw_chunks(rows, N, K);
+    a.rows_per_chunk = (int)((rows + chunks - 1) / chunks);
+    a.x = x; a.gamma = gamma; a.beta = beta; a.mean = mean; a.rstd = rstd; a.dy = dy;
+    a.part = static_cast<float*>(workspace);
+    const dim3 grid((unsigned)((N + enc::BN - 1) / enc::BN), (unsigned)((K + 1 + enc::BN - 1) / enc::BN),
+                    (unsigned)chunks);
+    if (a.ln) enc::rowgemm_dw_kernel<true><<<grid, 256, 0, s>>>(a);
+    else enc::rowgemm_dw_kernel<false><<<grid, 256, 0, s>>>(a);
+    int rc = launch_status("rowgemm_dw");
+    if (rc) return rc;
+    // dW = columns [0, N K), db = [N K, N K + N) (a null db drops them)
+    enc::chunk_sum(a.part, chunks, N * K + N, N * K, dw, db, s);
+    return launch_status("rowgemm_dw_sum");
+}
+
+size_t enc_row_ln_bwd_workspace(int64_t rows, int C) {
+    int64_t blocks = (rows + 3) / 4;
+    if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
+    return (size_t)blocks * 2 * C * sizeof(float);
+}
+
+int enc_row_ln_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
+                   const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                   float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s) {
+    enc::LNBArgs a{};
+    a.rows = rows; a.lddxn = lddxn; a.ldx = ldx; a.ldres = ldres; a.lddx = lddx; a.C = C;
+    a.dxn = dxn; a.x = x; a.gamma = gamma; a.mean = mean; a.rstd = rstd; a.dres = dres; a.dx = dx;
+    a.part = static_cast<float*>(workspace);
+    int64_t blocks = (rows + 3) / 4;
+    if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
+    if (dres != nullptr) enc::row_ln_bwd_kernel<true><<<(unsigned)blocks, 256, 0, s>>>(a);
+    else enc::row_ln_bwd_kernel<false><<<(unsigned)blocks, 256, 0, s>>>(a);
+    int rc = launch_status("row_layernorm_bwd");
+    if (rc) return rc;
+    enc::chunk_sum(a.part, (int)blocks, 2 * C, C, dgamma, dbeta, s);
+    return launch_status("row_layernorm_bwd_sum");
+}
+
+}  // namespace mmni
+
 extern "C" size_t mmni_rowgemm_dw_workspace_bytes(const mmni_rowgemm_desc* d) {
     if (d == nullptr || d->rows <= 0 || d->K <= 0 || d->N <= 0) return 0;
-    return (size_t)enc::dw_chunks(d->rows, d->N, d->K) * ((size_t)d->N * d->K + d->N) * sizeof(float);
+    return enc_rowgemm_dw_workspace(d->rows, d->N, d->K);
 }
 
 extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const float* gamma, const float* beta,
@@ -598,26 +651,12 @@ extern "C" int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const
     MMNI_ARG_CHECK(d->rows > 0 && d->K > 0 && d->N > 0, "rowgemm_dw: bad extents");
     MMNI_ARG_CHECK(d->ldx >= d->K && d->ldy >= d->N, "rowgemm_dw: leading dimensions below K / N (ldy: dY)");
     MMNI_ARG_CHECK(!d->ln || (gamma && beta && mean && rstd), "rowgemm_dw: LayerNorm recompute needs its inputs");
-    enc::DWArgs a{};
-    a.rows = d->rows; a.ldx = d->ldx; a.lddy = d->ldy; a.K = d->K; a.N = d->N; a.ln = d->ln;
-    const int chunks = enc::dw_chunks(d->rows, d->N, d->K);
-    a.rows_per_chunk = (int)((d->rows + chunks - 1) / chunks);
-    a.x = x; a.gamma = gamma; a.beta = beta; a.mean = mean; a.rstd = rstd; a.dy = dy;
-    a.part = static_cast<float*>(workspace);
-    const dim3 grid((unsigned)((d->N + enc::BN - 1) / enc::BN), (unsigned)((d->K + 1 + enc::BN - 1) / enc::BN),
-                    (unsigned)chunks);
-    if (d->ln) enc::rowgemm_dw_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-    else enc::rowgemm_dw_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-    int rc = launch_status("rowgemm_dw");
-    if (rc) return rc;
-    // dW = columns [0, N K), db = [N K, N K + N) (a null db drops them)
-    enc::chunk_sum(a.part, chunks, d->N * d->K + d->N, d->N * d->K, dw, db, (hipStream_t)stream);
-    return launch_status("rowgemm_dw_sum");
+    return enc_rowgemm_dw(d->rows, d->N, d->K, x, d->ldx, dy, d->ldy, d->ln ? gamma : nullptr, beta, mean, rstd, dw,
+                          db, workspace, (hipStream_t)stream);
 }
 
 extern "C" size_t mmni_row_layernorm_bwd_workspace_bytes(int64_t rows, int C) {
-    (void)rows;
-    return (size_t)enc::kLnbBlocks * 2 * C * sizeof(float);
+    return enc_row_ln_bwd_workspace(rows, C);
 }
 
 extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x,
@@ -629,16 +668,6 @@ extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int
     MMNI_ARG_CHECK(rows > 0 && C > 0 && C <= 256, "row_layernorm_bwd: C=%d outside 1..256", C);
     MMNI_ARG_CHECK(lddxn >= C && ldx >= C && lddx >= C && (dres == nullptr || ldres >= C),
                    "row_layernorm_bwd: leading dimensions below C");
-    enc::LNBArgs a{};
-    a.rows = rows; a.lddxn = lddxn; a.ldx = ldx; a.ldres = ldres; a.lddx = lddx; a.C = C;
-    a.dxn = dxn; a.x = x; a.gamma = gamma; a.mean = mean; a.rstd = rstd; a.dres = dres; a.dx = dx;
-    a.part = static_cast<float*>(workspace);
-    int64_t blocks = (rows + 3) / 4;
-    if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
-    if (dres != nullptr) enc::row_ln_bwd_kernel<true><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
-    else enc::row_ln_bwd_kernel<false><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(a);
-    int rc = launch_status("row_layernorm_bwd");
-    if (rc) return rc;
-    enc::chunk_sum(a.part, (int)blocks, 2 * C, C, dgamma, dbeta, (hipStream_t)stream);
-    return launch_status("row_layernorm_bwd_sum");
+    return enc_row_ln_bwd(rows, C, dxn, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma, dbeta,
+                          workspace, (hipStream_t)stream);
 }

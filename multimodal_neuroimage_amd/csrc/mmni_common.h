@@ -52,4 +52,17 @@ struct ColSegs {
 };
 void column_sum_segs(const float* part, int nparts, int ncols, const ColSegs& segs, hipStream_t s);
 
+// Row-GEMM weight gradient and row LayerNorm backward (encoder.hip), also used by the token ops
+// for short row counts (a few hundred to ~64k rows: the deep Swin stages), where the row-chunk
+// grid keeps many workgroups busy.  Workspace bytes first; the launches return 0 / hipError.
+size_t enc_rowgemm_dw_workspace(int64_t rows, int N, int K);
+int enc_rowgemm_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy, int64_t lddy,
+                   const float* gamma, const float* beta, const float* mean, const float* rstd, float* dw, float* db,
+                   void* workspace, hipStream_t s);
+size_t enc_row_ln_bwd_workspace(int64_t rows, int C);
+int enc_row_ln_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
+                   const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                   float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s);
+constexpr int64_t kSmallRows = 65536;   // token ops at or below this row count take the encoder kernels
+
 }  // namespace mmni

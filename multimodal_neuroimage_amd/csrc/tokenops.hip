@@ -359,7 +359,9 @@ extern "C" int mmni_layernorm_fwd(int64_t rows, int C, const float* x, const flo
 }
 
 extern "C" size_t mmni_layernorm_bwd_workspace_bytes(int64_t rows, int C) {
-    return (size_t)ln_grid(rows) * 2 * C * sizeof(float);
+    const size_t own = (size_t)ln_grid(rows) * 2 * C * sizeof(float);
+    const size_t small = rows <= kSmallRows ? enc_row_ln_bwd_workspace(rows, C) : 0;
+    return own > small ? own : small;
 }
 
 extern "C" int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const float* x, const float* gamma,
@@ -370,6 +372,9 @@ extern "C" int mmni_layernorm_bwd(int64_t rows, int C, const float* dy, const fl
     MMNI_ARG_CHECK(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(dy) % 16 == 0 &&
                        reinterpret_cast<uintptr_t>(dx) % 16 == 0,
                    "layernorm_bwd: tensors must be 16-byte aligned");
+    if (rows <= kSmallRows && C <= 256)   // a wave per row: one lane per row left a short call serial
+        return enc_row_ln_bwd(rows, C, dy, C, x, C, gamma, mean, rstd, nullptr, 0, dx, C, dgamma, dbeta, workspace,
+                              (hipStream_t)stream);
     const int grid = ln_grid(rows);
     float* part = reinterpret_cast<float*>(workspace);
     MMNI_LN_DISPATCH(layernorm_bwd_kernel, rows, dy, x, gamma, mean, rstd, dx, part)
@@ -392,13 +397,17 @@ static int dw_waves_for(int64_t rows) {
 }
 
 extern "C" size_t mmni_linear_dw_workspace_bytes(int N, int K) {
-    return (size_t)(dw_waves() / 4) * (N * K + N) * sizeof(float);   // per-block partials
+    // per-block partials; covers the short-row path too (at most 256 row chunks)
+    return (size_t)(dw_waves() / 4) * (N * K + N) * sizeof(float);
 }
 
 extern "C" int mmni_linear_dw(int64_t rows, int N, int K, const float* x, int64_t ldx, const float* dy,
                               int64_t lddy, float* dw, float* db, void* workspace, void* stream) {
     MMNI_ARG_CHECK(rows > 0 && N > 0 && K > 0 && x && dy && dw && workspace, "linear_dw: bad arguments");
     MMNI_ARG_CHECK(ldx >= K && lddy >= N, "linear_dw: leading dimensions too small");
+    if (rows <= kSmallRows)   // row chunks x 64 x 64 output tiles: many workgroups for a short call
+        return enc_rowgemm_dw(rows, N, K, x, ldx, dy, lddy, nullptr, nullptr, nullptr, nullptr, dw, db, workspace,
+                              (hipStream_t)stream);
     const int NT = (N + 15) / 16, KT = (K + 15) / 16;
     float* part = reinterpret_cast<float*>(workspace);
     const int waves = dw_waves_for(rows);

@@ -32,25 +32,47 @@
 namespace mmni {
 
 // max|dout| and max|v| for the fixed-point bound (non-negative float bits order as uints).
-// dout == nullptr: v only; v == nullptr: dout only.
-__global__ void wattn_absmax_kernel(const float* dout, long long os, const float* v, long long vs, long long T,
-                                    int C, unsigned int* maxbits) {
+// dout == nullptr: v only; v == nullptr: dout only.  Rows in a grid-stride loop (no 64-bit
+// division per element), the block's maximum through LDS, ONE atomic per block and word (per-wave
+// atomics on one word serialise at the L2: 4,096 of them cost ~48 us).
+__global__ __launch_bounds__(256) void wattn_absmax_kernel(const float* dout, long long os, const float* v,
+                                                           long long vs, long long T, int C,
+                                                           unsigned int* maxbits) {
+    __shared__ float red[2][4];
     float md = 0.f, mv = 0.f;
-    const long long n = T * C;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-        const long long r = i / C;
-        const int c = (int)(i - r * C);
-        if (dout) md = fmaxf(md, fabsf(dout[r * os + c]));
-        if (v) mv = fmaxf(mv, fabsf(v[r * vs + c]));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // a wave covers rpw whole rows per step (C <= 64: lane = sub-row * C + c) or one row in 64-lane
+    // pieces (C > 64)
+    const int rpw = C <= 64 ? 64 / C : 1;
+    const int sub = C <= 64 ? lane / C : 0, c0 = C <= 64 ? lane - sub * C : lane, cstep = C <= 64 ? C : 64;
+    if (sub < rpw) {
+        const long long nw = (long long)gridDim.x * 4 * rpw;
+#pragma unroll 4
+        for (long long r = ((long long)blockIdx.x * 4 + wave) * rpw + sub; r < T; r += nw) {
+            for (int c = c0; c < C; c += cstep) {
+                if (dout) md = fmaxf(md, fabsf(dout[r * os + c]));
+                if (v) mv = fmaxf(mv, fabsf(v[r * vs + c]));
+            }
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         md = fmaxf(md, __shfl_xor(md, o));
         mv = fmaxf(mv, __shfl_xor(mv, o));
     }
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) { red[0][wave] = md; red[1][wave] = mv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        md = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+        mv = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
         if (dout) atomicMax(&maxbits[0], __float_as_uint(md));
         if (v) atomicMax(&maxbits[1], __float_as_uint(mv));
     }
+}
+
+// blocks of the generic scan: ~16 elements per lane, at most 2,048 blocks (one atomic each)
+static unsigned absmax_blocks(long long T, int C) {
+    long long b = (T * C + 4095) / 4096;
+    return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
 
 // max|dout| over a contiguous, 16-byte aligned array of n4 float4 (the common case: dout rows of
@@ -783,7 +805,8 @@ extern "C" int mmni_wattn_fwd(const mmni_wattn_desc* d, const float* q, const fl
     if (e != hipSuccess) { set_error("wattn_fwd launch: %s", hipGetErrorString(e)); return (int)e; }
     if (vmax && !packed) {   // generic kernels: a separate pass over v (vmax is maxbits[1]-shaped: pass vmax - 1)
         const long long T = (long long)a.g.nwin * a.g.N;
-        wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(nullptr, 0, v, d->v_stride, T, d->C, vmax - 1);
+        wattn_absmax_kernel<<<absmax_blocks(T, d->C), 256, 0, (hipStream_t)stream>>>(nullptr, 0, v, d->v_stride, T, d->C,
+                                                                               vmax - 1);
         return launch_status("wattn_absmax_v");
     }
     return 0;
@@ -856,8 +879,8 @@ extern "C" int mmni_wattn_bwd(const mmni_wattn_desc* d, const float* q, const fl
         wattn_absmax_dout4_kernel<<<(unsigned)blocks, 1024, 0, (hipStream_t)stream>>>(
             reinterpret_cast<const float4*>(dout), n4, vmax, a.maxbits);
     } else {
-        wattn_absmax_kernel<<<1024, 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T, d->C,
-                                                                   a.maxbits);
+        wattn_absmax_kernel<<<absmax_blocks(T, d->C), 256, 0, (hipStream_t)stream>>>(dout, d->o_stride, v, d->v_stride, T,
+                                                                               d->C, a.maxbits);
     }
     rc = launch_status("wattn_absmax");
     if (rc) return rc;
