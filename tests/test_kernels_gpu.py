@@ -366,7 +366,7 @@ def test_layernorm_fwd_bwd_vs_torch_fp64(device, rows, C):
 
 
 LIN = [(5000, 12, 36), (4097, 12, 12), (3001, 12, 48), (3001, 48, 12), (2000, 48, 144), (1000, 24, 72), (777, 96, 48),
-       (108, 48, 192), (13, 12, 12), (65, 24, 96)]
+       (108, 48, 192), (13, 12, 12), (65, 24, 96), (70001, 12, 36)]
 
 
 @pytest.mark.parametrize("rows,K,N", LIN)
