@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 6
+#define MMNI_ABI_VERSION 7
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -370,6 +370,22 @@ int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn,
                            const float* gamma, const float* mean, const float* rstd, const float* dres,
                            int64_t ldres, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace,
                            void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Swin-V2 continuous position bias table (ABI v7; replaces WindowAttention.cpb_mlp applied to
+ * relative_coords_table and the 16 * sigmoid that follows, swin_v2_module.py:88-91,158-162):
+ *   out[t][h] = 16 * sigmoid( sum_j w2[h][j] * relu( w1[j] . coords[t] + b1[j] ) )
+ *   coords (tsz, nd), w1 (hidden, nd), b1 (hidden), w2 (heads, hidden), out (tsz, heads);
+ *   nd <= 3, hidden <= 1024, heads <= 32, fp32.
+ *   mmni_cpb_bwd  dw1, db1, dw2 from dout and the forward's out (per-block partial rows, fixed-order
+ *                 column sum: deterministic; the coordinate table is a constant buffer: no dcoords).
+ * ------------------------------------------------------------------------------------ */
+int mmni_cpb_fwd(int64_t tsz, int nd, int hidden, int heads, const float* coords, const float* w1, const float* b1,
+                 const float* w2, float* out, void* stream);
+size_t mmni_cpb_bwd_workspace_bytes(int64_t tsz, int nd, int hidden, int heads);
+int mmni_cpb_bwd(int64_t tsz, int nd, int hidden, int heads, const float* coords, const float* w1, const float* b1,
+                 const float* w2, const float* out, const float* dout, float* dw1, float* db1, float* dw2,
+                 void* workspace, void* stream);
 
 int mmni_version(void);
 const char* mmni_last_error(void);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -76,6 +76,9 @@ SIGNATURES = {
     "mmni_rowgemm_dw_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RowGemmDesc)]),
     "mmni_rowgemm_dw": (_c_int, [ctypes.POINTER(RowGemmDesc)] + [_vp] * 10),
     "mmni_row_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
+    "mmni_cpb_fwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 6),
+    "mmni_cpb_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int, _c_int, _c_int]),
+    "mmni_cpb_bwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 11),
     "mmni_row_layernorm_bwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp,
                                         _c_i64, _vp, _vp, _vp, _vp]),
     "mmni_last_error": (ctypes.c_char_p, []),

@@ -997,6 +997,44 @@ def _rows_view(t, C):
     return t2
 
 
+class _CpbTable(torch.autograd.Function):
+    """16 * sigmoid(cpb_mlp(relative_coords_table)) for a Swin-V2 WindowAttention
+    (swin_v2_module.py:88-91,158-162) in one HIP launch per direction (mmni_cpb_fwd / _bwd, cpb.hip):
+    Linear(nd, hidden) -> ReLU -> Linear(hidden, heads, no bias) -> 16 * sigmoid.  The coordinate
+    table is a constant buffer (no gradient); dW1 / db1 / dW2 are fixed-order sums (deterministic)."""
+
+    @staticmethod
+    def forward(ctx, coords, w1, b1, w2):
+        require_device(coords, w1, b1, w2)
+        coords = coords.reshape(-1, coords.shape[-1]).contiguous()
+        w1, b1, w2 = w1.contiguous(), b1.contiguous(), w2.contiguous()
+        tsz, nd = coords.shape
+        hidden, heads = w1.shape[0], w2.shape[0]
+        out = torch.empty(tsz, heads, device=coords.device, dtype=torch.float32)
+        check(_lib.load().mmni_cpb_fwd(tsz, nd, hidden, heads, ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(out),
+                                       stream_handle(coords.device)), "mmni_cpb_fwd")
+        ctx.save_for_backward(coords, w1, b1, w2, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        coords, w1, b1, w2, out = ctx.saved_tensors
+        tsz, nd = coords.shape
+        hidden, heads = w1.shape[0], w2.shape[0]
+        dout = dout.contiguous()
+        dw1, db1, dw2 = torch.empty_like(w1), torch.empty_like(b1), torch.empty_like(w2)
+        L = _lib.load()
+        ws = _workspace(L.mmni_cpb_bwd_workspace_bytes(tsz, nd, hidden, heads), coords.device)
+        check(L.mmni_cpb_bwd(tsz, nd, hidden, heads, ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(out), ptr(dout),
+                             ptr(dw1), ptr(db1), ptr(dw2), ptr(ws), stream_handle(coords.device)), "mmni_cpb_bwd")
+        return None, dw1, db1, dw2
+
+
+def cpb_table(coords, w1, b1, w2):
+    """(tsz, heads) = 16 * sigmoid(W2 relu(W1 coords + b1)) on the HIP kernels (fp32)."""
+    return _CpbTable.apply(coords, w1, b1, w2)
+
+
 def rowgemm(x2, w, bias=None, *, ln=None, relu=False, aux=None, res=None, transpose_w=False, stats=False):
     """y = epi(x' W^T) on token rows with the HIP row-GEMM (mmni_rowgemm).
 

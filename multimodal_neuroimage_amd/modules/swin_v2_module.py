@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
-from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear, mlp
+from ..functional import window_attention_self, conv3d_cl, LN100, layer_norm, linear, mlp, cpb_table
 from ._common import (DropPath, to_2tuple, to_ntuple, trunc_normal_, relative_index_buffer, shift_mask_buffer,
                       attend_masked_windows, clamp_window, geometry, patch_merge_gather)
 
@@ -91,9 +91,10 @@ class WindowAttention(nn.Module):
         self.softmax = nn.Softmax(dim=-1)
 
     def bias_table(self):
-        """16*sigmoid(cpb_mlp(relative_coords_table)) as a (Tsz, heads) table (swin_v2_module.py:158-162)."""
-        t = self.cpb_mlp(self.relative_coords_table).view(-1, self.num_heads_swin)
-        return 16 * torch.sigmoid(t)
+        """16*sigmoid(cpb_mlp(relative_coords_table)) as a (Tsz, heads) table (swin_v2_module.py:158-162),
+        one HIP launch per direction (functional.cpb_table)."""
+        l1, l2 = self.cpb_mlp[0], self.cpb_mlp[2]
+        return cpb_table(self.relative_coords_table, l1.weight, l1.bias, l2.weight)
 
     def tau(self):
         """exp(min(logit_scale, ln 100)) per head (swin_v2_module.py:154-155)."""

@@ -763,3 +763,34 @@ def test_crossmodal_model_trains_with_reference_dropout_defaults(device):
                 mod.attn_dropout = 0.0
         b = m(xl, xu)["binary_classification"]
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("window,heads", [((6, 6, 6), 3), ((6, 6, 6), 24), ((3, 3, 3), 12), ((7, 7), 6), ((2, 2, 2), 32)])
+def test_cpb_table_vs_torch_fp64_and_deterministic(device, window, heads):
+    """16 * sigmoid(cpb_mlp(relative_coords_table)) (swin_v2_module.py:158-162) on mmni_cpb_fwd /
+    _bwd against the same MLP in torch float64: table 1e-5, dW1 / db1 / dW2 1e-5 max-rel, and bitwise
+    repeatable gradients."""
+    from multimodal_neuroimage_amd.modules.swin_v2_module import _coords_table
+    nd = len(window)
+    coords = _coords_table(window, (0,) * nd).to(device)
+    g = torch.Generator().manual_seed(heads + nd)
+    w1 = (torch.randn(512, nd, generator=g) * 0.5).to(device)
+    b1 = (torch.randn(512, generator=g) * 0.5).to(device)
+    w2 = (torch.randn(heads, 512, generator=g) * 0.05).to(device)
+    dout = torch.randn(coords.reshape(-1, nd).shape[0], heads, generator=g).to(device)
+    leaves = [t.double().clone().requires_grad_(True) for t in (w1, b1, w2)]
+    c64 = coords.reshape(-1, nd).double()
+    ref = 16 * torch.sigmoid(torch.relu(c64 @ leaves[0].t() + leaves[1]) @ leaves[2].t())
+    ref.backward(dout.double())
+    runs = []
+    for _ in range(2):
+        ps = [t.clone().requires_grad_(True) for t in (w1, b1, w2)]
+        out = MF.cpb_table(coords, *ps)
+        out.backward(dout)
+        torch.cuda.synchronize()
+        runs.append((out.detach(), [p.grad for p in ps]))
+    out, grads = runs[0]
+    assert rel_err(out, ref) < 1e-5
+    for got, leaf in zip(grads, leaves):
+        assert rel_err(got, leaf.grad) < 1e-5
+    assert all(torch.equal(a, b) for a, b in zip(runs[0][1], runs[1][1]))
