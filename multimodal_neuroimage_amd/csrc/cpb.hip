@@ -12,8 +12,9 @@ namespace mmni {
 namespace cpb {
 
 constexpr int kMaxHeads = 32, kMaxHidden = 1024, kMaxNd = 3;
-constexpr int kEpb = 4;          // table entries per forward block
-constexpr int kBwdBlocks = 64;   // backward partial rows
+constexpr int kEpb = 16;         // table entries per forward block
+constexpr int kBwdBlocks = 128;  // backward partial rows
+constexpr int kHpw = kMaxHeads / 4;   // heads per wave in the forward (4 waves)
 
 struct Args {
     int64_t tsz;
@@ -28,8 +29,9 @@ struct Args {
     float* part;           // backward: [block][heads * hidden | hidden * nd | hidden]
 };
 
-// hidden activations of kEpb entries in LDS, then one wave per (entry, head) dot product over the
-// hidden units (64 lanes x hidden / 64 products, butterfly sum: fixed order)
+// hidden activations of kEpb entries in LDS; wave w owns heads w, w + 4, ...: their W2 rows are
+// loaded once into registers (every load in flight together), then each (entry, head) output is a
+// 64-lane dot over the hidden units with a butterfly sum (fixed order)
 __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
     __shared__ float h[kEpb][kMaxHidden];
     const int64_t e0 = (int64_t)blockIdx.x * kEpb;
@@ -42,15 +44,32 @@ __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
         }
         h[e][j] = fmaxf(z, 0.f);
     }
-    __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int o = wave; o < kEpb * a.heads; o += 4) {
-        const int e = o / a.heads, hd = o - e * a.heads;
-        if (e0 + e >= a.tsz) continue;   // wave-uniform
-        float s = 0.f;
-        for (int j = lane; j < a.hidden; j += 64) s = fmaf(a.w2[hd * a.hidden + j], h[e][j], s);
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if (lane == 0) a.y[(e0 + e) * a.heads + hd] = 16.f / (1.f + expf(-s));
+    constexpr int JPL = kMaxHidden / 64;   // hidden units per lane (upper bound)
+    float w2r[kHpw][JPL];
+#pragma unroll
+    for (int u = 0; u < kHpw; ++u) {
+        const int hd = wave + 4 * u;
+#pragma unroll
+        for (int i = 0; i < JPL; ++i) {
+            const int j = lane + 64 * i;
+            w2r[u][i] = (hd < a.heads && j < a.hidden) ? a.w2[hd * a.hidden + j] : 0.f;
+        }
+    }
+    __syncthreads();
+    const int ne = e0 + kEpb <= a.tsz ? kEpb : (int)(a.tsz - e0);
+#pragma unroll
+    for (int u = 0; u < kHpw; ++u) {
+        const int hd = wave + 4 * u;
+        if (hd >= a.heads) break;   // wave-uniform
+        for (int e = 0; e < ne; ++e) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < JPL; ++i)
+                if (lane + 64 * i < a.hidden) s = fmaf(w2r[u][i], h[e][lane + 64 * i], s);
+            for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+            if (lane == 0) a.y[(e0 + e) * a.heads + hd] = 16.f / (1.f + expf(-s));
+        }
     }
 }
 
@@ -62,7 +81,7 @@ constexpr int kChunk = 64;       // backward entries staged in LDS per round
 
 template <int U>
 __global__ __launch_bounds__(256) void cpb_bwd_kernel(Args a) {
-    __shared__ float dz[kChunk][kMaxHeads];
+    __shared__ __attribute__((aligned(16))) float dz[kChunk][kMaxHeads];
     __shared__ float cs[kChunk][kMaxNd];
     float w2c[U][kMaxHeads], w1r[U][kMaxNd], b1r[U];
     float gw2[U][kMaxHeads], gw1[U][kMaxNd], gb1[U];
@@ -91,10 +110,14 @@ __global__ __launch_bounds__(256) void cpb_bwd_kernel(Args a) {
     for (int64_t c0 = e_begin; c0 < e_end; c0 += kChunk) {
         const int n = (int)(e_end - c0 < kChunk ? e_end - c0 : kChunk);
         __syncthreads();   // the previous chunk is consumed
-        for (int i = threadIdx.x; i < n * a.heads; i += 256) {
-            const int e = i / a.heads, h = i - e * a.heads;
-            const float o = a.out[(c0 + e) * a.heads + h];
-            dz[e][h] = a.dout[(c0 + e) * a.heads + h] * o * (1.f - o * (1.f / 16.f));   // d(16 sigmoid)
+        for (int i = threadIdx.x; i < n * kMaxHeads; i += 256) {
+            const int e = i / kMaxHeads, h = i - e * kMaxHeads;
+            float v = 0.f;   // heads past a.heads: zero pad (read by the float4 loads)
+            if (h < a.heads) {
+                const float o = a.out[(c0 + e) * a.heads + h];
+                v = a.dout[(c0 + e) * a.heads + h] * o * (1.f - o * (1.f / 16.f));   // d(16 sigmoid)
+            }
+            dz[e][h] = v;
         }
         for (int i = threadIdx.x; i < n * a.nd; i += 256) cs[i / a.nd][i % a.nd] = a.coords[c0 * a.nd + i];
         __syncthreads();
@@ -107,10 +130,15 @@ __global__ __launch_bounds__(256) void cpb_bwd_kernel(Args a) {
                 const float hj = fmaxf(z, 0.f);
                 float dh = 0.f;
 #pragma unroll
-                for (int h = 0; h < kMaxHeads; ++h) {
-                    const float g = h < a.heads ? dz[e][h] : 0.f;
-                    dh = fmaf(w2c[u][h], g, dh);
-                    gw2[u][h] = fmaf(g, hj, gw2[u][h]);
+                for (int h4 = 0; h4 < kMaxHeads; h4 += 4) {
+                    if (h4 >= a.heads) break;   // uniform; heads past a.heads read the zeroed pad
+                    const float4 g4 = *reinterpret_cast<const float4*>(&dz[e][h4]);
+                    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        dh = fmaf(w2c[u][h4 + i], g[i], dh);
+                        gw2[u][h4 + i] = fmaf(g[i], hj, gw2[u][h4 + i]);
+                    }
                 }
                 dh = z > 0.f ? dh : 0.f;
 #pragma unroll

@@ -586,9 +586,7 @@ class _TokenLinear(torch.autograd.Function):
         if _tlin_ok(K, N):
             y = _tlin(x2, weight, bias, K, N, residual=r2)
         else:
-            y = F.linear(x2, weight, bias)
-            if r2 is not None:
-                y = y + r2
+            y = rowgemm(x2.contiguous(), weight.contiguous(), bias, res=r2)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -602,7 +600,8 @@ class _TokenLinear(torch.autograd.Function):
             dx, dw, db = _linear_bwd_fused(x2, dy2, weight, ctx.has_bias)
             return dx.view(ctx.xshape), dw, db, (dy if ctx.needs_input_grad[3] else None)
         if ctx.needs_input_grad[0]:
-            dx = _tlin(dy2, weight, None, N, K, transposed=True) if _tlin_ok(N, K) else dy2 @ weight
+            dx = (_tlin(dy2, weight, None, N, K, transposed=True) if _tlin_ok(N, K)
+                  else rowgemm(dy2.contiguous(), weight.contiguous(), transpose_w=True))
             dx = dx.view(ctx.xshape)
         dw, db = _linear_dw(x2, dy2, N, K, ctx.has_bias)
         return dx, dw, db, (dy if ctx.needs_input_grad[3] else None)
@@ -908,9 +907,34 @@ def linear(x, lin_or_weight, bias=None, residual=None):
     require_device(x, what="linear")
     N, K = weight.shape
     if ((N + 15) // 16, (K + 15) // 16) not in _DW_TILES or K % 4:
-        y = F.linear(x, weight, bias)
-        return y if residual is None else residual + y
+        return _RowLinear.apply(x, weight, bias, residual)   # any shape, fp32, on the row-GEMM kernels
     return _TokenLinear.apply(x, weight, bias, residual)
+
+
+class _RowLinear(torch.autograd.Function):
+    """y = x W^T + b (+ residual) for the token-Linear shapes the tiled token kernels do not
+    compile (the Swin-V2 deep stages' widths, PatchMerging reductions, heads): forward and dX on
+    mmni_rowgemm, dW / db on mmni_rowgemm_dw (deterministic).  These ran as one-workgroup library
+    GEMMs of ~11-13 us each at the deep stages' few hundred rows."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual):
+        N, K = weight.shape
+        x2 = _rows2d(x, K).contiguous()
+        r2 = residual.reshape(-1, N).contiguous() if residual is not None else None
+        y = rowgemm(x2, weight.contiguous(), bias, res=r2)
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias, ctx.xshape, ctx.has_res = bias is not None, x.shape, residual is not None
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        N, K = weight.shape
+        dy2 = _rows2d(dy, N).contiguous()
+        dx = rowgemm(dy2, weight.contiguous(), transpose_w=True).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw, db = rowgemm_dw(x2, dy2, N, K, ctx.has_bias)
+        return dx, dw, db, (dy if ctx.has_res and ctx.needs_input_grad[3] else None)
 
 
 # ------------------------------------------------------------------------------------------
