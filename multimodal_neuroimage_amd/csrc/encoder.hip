@@ -116,37 +116,37 @@ struct Tile {
     }
 };
 
-// Plain rows: X and W stream through an SDEPTH-slot register ring.  Whole laps of SDEPTH groups run
-// in a loop with no exits (a slot is refilled right after its MFMAs, so the ring keeps its
-// registers and the wait before each group leaves the other SDEPTH - 1 groups in flight), the
-// NG % SDEPTH tail after it.
-template <bool VEC, bool TW>
+// Plain rows: X and W stream through a D-slot register ring over groups [g0, g0 + ng).  Whole laps
+// of D groups run in a loop with no exits (a slot is refilled right after its MFMAs, so the ring
+// keeps its registers and the wait before each group leaves the other D - 1 groups in flight), the
+// ng % D tail after it.
+template <bool VEC, bool TW, int D>
 __device__ __forceinline__ void stream_rows(const RGArgs& a, Tile& T, int64_t ra, int64_t rb, bool oka, bool okb,
-                                            int na, int nb, int g, int NG) {
-    f4 xa[SDEPTH], xb[SDEPTH], wa[SDEPTH], wb[SDEPTH];
+                                            int na, int nb, int g, int g0, int ng) {
+    f4 xa[D], xb[D], wa[D], wb[D];
 #pragma unroll
-    for (int d = 0; d < SDEPTH; ++d) {
-        const int k0 = KG * d + 4 * g;   // groups past K load as zeros
+    for (int d = 0; d < D; ++d) {
+        const int k0 = KG * (g0 + d) + 4 * g;   // groups past K load as zeros
         xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
         xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
         wa[d] = load_w4<VEC, TW>(a, na, k0);
         wb[d] = load_w4<VEC, TW>(a, nb, k0);
     }
-    const int laps = NG / SDEPTH;
+    const int laps = ng / D;
     for (int l = 0; l < laps; ++l) {
 #pragma unroll
-        for (int d = 0; d < SDEPTH; ++d) {
+        for (int d = 0; d < D; ++d) {
             T.group(xa[d], xb[d], wa[d], wb[d]);
-            const int k0 = KG * ((l + 1) * SDEPTH + d) + 4 * g;
+            const int k0 = KG * (g0 + (l + 1) * D + d) + 4 * g;
             xa[d] = load_k4<VEC>(a.x, ra, a.ldx, oka, k0, a.K);
             xb[d] = load_k4<VEC>(a.x, rb, a.ldx, okb, k0, a.K);
             wa[d] = load_w4<VEC, TW>(a, na, k0);
             wb[d] = load_w4<VEC, TW>(a, nb, k0);
         }
     }
-    const int rem = NG - laps * SDEPTH;
+    const int rem = ng - laps * D;
 #pragma unroll
-    for (int d = 0; d < SDEPTH - 1; ++d)
+    for (int d = 0; d < D - 1; ++d)
         if (d < rem) T.group(xa[d], xb[d], wa[d], wb[d]);
 }
 
@@ -215,16 +215,25 @@ __device__ __forceinline__ void ln_rows(const RGArgs& a, Tile& T, int64_t ra, in
     }
 }
 
-template <bool LN, bool VEC, bool TW>
+// KS = 1: a workgroup owns 64 rows x 64 outputs (2 x 2 waves of 32 x 32).  KS = 2 / 4 (long K, few
+// output tiles): the 4 waves split K instead — 32 rows x 64 outputs with 2 K-halves, or 32 x 32 with
+// 4 K-quarters — and the partial tiles are added through LDS in K order (deterministic), so a
+// 6,912-row GEMM with N = 84 runs ~2,600 waves instead of ~650.
+template <bool LN, bool VEC, bool TW, int KS>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t = lane & 15, g = lane >> 4;
-    const int64_t m0 = (int64_t)blockIdx.x * BM + (wave & 1) * 32;     // the wave's 32 rows
-    const int n0 = blockIdx.y * BN + (wave >> 1) * 32;                 // and 32 outputs
+    constexpr int BMK = KS == 1 ? 64 : 32, BNK = KS == 4 ? 32 : 64;
+    const int mw = KS == 1 ? (wave & 1) : 0;
+    const int nw = KS == 1 ? (wave >> 1) : (KS == 2 ? (wave & 1) : 0);
+    const int kp = KS == 1 ? 0 : (KS == 2 ? (wave >> 1) : wave);
+    const int64_t m0 = (int64_t)blockIdx.x * BMK + mw * 32;             // the wave's 32 rows
+    const int n0 = blockIdx.y * BNK + nw * 32;                         // and 32 outputs
     const int64_t ra = m0 + t, rb = m0 + 16 + t;                       // A rows of the two m tiles
     const bool oka = ra < a.rows, okb = rb < a.rows;
     const int na = n0 + t, nb = n0 + 16 + t;                           // B columns of the two n tiles
-    if (m0 >= a.rows || n0 >= a.N) return;   // a wave wholly past the edge (no barriers here)
+    const bool active = m0 < a.rows && n0 < a.N;
+    if (KS == 1 && !active) return;   // a wave wholly past the edge (KS = 1 has no barrier)
     const int NG = (a.K + KG - 1) / KG;
     Tile T;
     T.zero();
@@ -237,8 +246,25 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RGArgs a) {
 #undef MMNI_LN_CASE
             default: break;   // K > KMAX_LN is refused by the host
         }
+    } else if constexpr (KS == 1) {
+        stream_rows<VEC, TW, SDEPTH>(a, T, ra, rb, oka, okb, na, nb, g, 0, NG);
     } else {
-        stream_rows<VEC, TW>(a, T, ra, rb, oka, okb, na, nb, g, NG);
+        const int per = (NG + KS - 1) / KS, g0 = kp * per;
+        const int ng = NG - g0 < per ? NG - g0 : per;
+        if (active && ng > 0) stream_rows<VEC, TW, DEPTH>(a, T, ra, rb, oka, okb, na, nb, g, g0, ng);
+        // K parts 1 .. KS-1 hand their tiles to part 0 through LDS; part 0 adds them in order
+        __shared__ f4 red[3][4][64];
+        const int slot = nw * (KS - 1) + kp - 1;
+        if (kp > 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) red[slot][i][lane] = T.acc[i >> 1][i & 1];
+        }
+        __syncthreads();
+        if (kp > 0 || !active) return;
+#pragma unroll
+        for (int p = 0; p < KS - 1; ++p)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) T.acc[i >> 1][i & 1] += red[nw * (KS - 1) + p][i][lane];
     }
     auto& acc = T.acc;
     // epilogue: D[row 4 g + i][col t] of tile (mi, ni).  The residual / ReLU-mask operands load
@@ -573,17 +599,34 @@ extern "C" int mmni_rowgemm(const mmni_rowgemm_desc* d, const float* x, const fl
     // 16-byte operand pieces when every row of x (and of a k-contiguous weight) starts aligned
     const bool vec = d->K % 4 == 0 && d->ldx % 4 == 0 && al(x) && (!d->ln || (al(gamma) && al(beta))) &&
                      (tw || (d->w_sn % 4 == 0 && al(w)));
-    const dim3 grid((unsigned)((d->rows + enc::BM - 1) / enc::BM), (unsigned)((d->N + enc::BN - 1) / enc::BN));
     hipStream_t s = (hipStream_t)stream;
-#define MMNI_RG(LN, VEC, TW) enc::rowgemm_kernel<LN, VEC, TW><<<grid, 256, 0, s>>>(a)
+    // K split across the workgroup's waves when the 32 x 32 output tiles alone leave the SIMDs
+    // mostly idle and K is long enough to share (<= 4 waves per SIMD in flight either way)
+    const int64_t tiles = ((d->rows + 31) / 32) * ((d->N + 31) / 32);
+    const int NG = (d->K + enc::KG - 1) / enc::KG;
+    int ks = 1;
+    if (!d->ln) {
+        if (tiles * 4 <= 4096 && NG >= 12) ks = 4;
+        else if (tiles * 2 <= 4096 && NG >= 6) ks = 2;
+    }
+    const int bm = ks == 1 ? 64 : 32, bn = ks == 4 ? 32 : 64;
+    const dim3 grid((unsigned)((d->rows + bm - 1) / bm), (unsigned)((d->N + bn - 1) / bn));
+#define MMNI_RG(LN, VEC, TW, KS) enc::rowgemm_kernel<LN, VEC, TW, KS><<<grid, 256, 0, s>>>(a)
+#define MMNI_RG_KS(VEC, TW)                                   \
+    do {                                                      \
+        if (ks == 4) MMNI_RG(false, VEC, TW, 4);              \
+        else if (ks == 2) MMNI_RG(false, VEC, TW, 2);         \
+        else MMNI_RG(false, VEC, TW, 1);                      \
+    } while (0)
     if (d->ln) {
         MMNI_ARG_CHECK(!tw, "rowgemm: the LayerNorm prologue takes a k-contiguous weight");
-        if (vec) MMNI_RG(true, true, false); else MMNI_RG(true, false, false);
+        if (vec) MMNI_RG(true, true, false, 1); else MMNI_RG(true, false, false, 1);
     } else if (tw) {
-        if (vec) MMNI_RG(false, true, true); else MMNI_RG(false, false, true);
+        if (vec) MMNI_RG_KS(true, true); else MMNI_RG_KS(false, true);
     } else {
-        if (vec) MMNI_RG(false, true, false); else MMNI_RG(false, false, false);
+        if (vec) MMNI_RG_KS(true, false); else MMNI_RG_KS(false, false);
     }
+#undef MMNI_RG_KS
 #undef MMNI_RG
     return launch_status("rowgemm");
 }
