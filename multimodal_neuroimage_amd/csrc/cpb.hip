@@ -34,15 +34,36 @@ struct Args {
 // 64-lane dot over the hidden units with a butterfly sum (fixed order)
 __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
     __shared__ float h[kEpb][kMaxHidden];
+    __shared__ float cs[kEpb][kMaxNd];
     const int64_t e0 = (int64_t)blockIdx.x * kEpb;
-    for (int i = threadIdx.x; i < kEpb * a.hidden; i += 256) {
-        const int e = i / a.hidden, j = i - e * a.hidden;
-        float z = 0.f;
-        if (e0 + e < a.tsz) {
-            z = a.b1[j];
-            for (int d = 0; d < a.nd; ++d) z = fmaf(a.w1[j * a.nd + d], a.coords[(e0 + e) * a.nd + d], z);
+    const int ne = e0 + kEpb <= a.tsz ? kEpb : (int)(a.tsz - e0);
+    if (threadIdx.x < kEpb * kMaxNd) {
+        const int e = threadIdx.x / kMaxNd, d = threadIdx.x - e * kMaxNd;
+        cs[e][d] = (e < ne && d < a.nd) ? a.coords[(e0 + e) * a.nd + d] : 0.f;
+    }
+    // a thread per hidden unit (up to 4 units): its W1 row and bias in registers, the entries'
+    // coordinates from LDS — no global load inside the entry loop
+    constexpr int UH = kMaxHidden / 256;
+    float w1r[UH][kMaxNd], b1r[UH];
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+        const int j = threadIdx.x + 256 * u;
+        const bool ok = j < a.hidden;
+#pragma unroll
+        for (int d = 0; d < kMaxNd; ++d) w1r[u][d] = (ok && d < a.nd) ? a.w1[j * a.nd + d] : 0.f;
+        b1r[u] = ok ? a.b1[j] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+        const int j = threadIdx.x + 256 * u;
+        if (j >= a.hidden) break;
+        for (int e = 0; e < kEpb; ++e) {
+            float z = b1r[u];
+#pragma unroll
+            for (int d = 0; d < kMaxNd; ++d) z = fmaf(w1r[u][d], cs[e][d], z);
+            h[e][j] = fmaxf(z, 0.f);
         }
-        h[e][j] = fmaxf(z, 0.f);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int JPL = kMaxHidden / 64;   // hidden units per lane (upper bound)
@@ -57,7 +78,6 @@ __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
         }
     }
     __syncthreads();
-    const int ne = e0 + kEpb <= a.tsz ? kEpb : (int)(a.tsz - e0);
 #pragma unroll
     for (int u = 0; u < kHpw; ++u) {
         const int hd = wave + 4 * u;
