@@ -376,7 +376,7 @@ int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn,
  * relative_coords_table and the 16 * sigmoid that follows, swin_v2_module.py:88-91,158-162):
  *   out[t][h] = 16 * sigmoid( sum_j w2[h][j] * relu( w1[j] . coords[t] + b1[j] ) )
  *   coords (tsz, nd), w1 (hidden, nd), b1 (hidden), w2 (heads, hidden), out (tsz, heads);
- *   nd <= 3, hidden <= 1024, heads <= 32, fp32.
+ *   nd <= 3, hidden <= 512, heads <= 32, fp32.
  *   mmni_cpb_bwd  dw1, db1, dw2 from dout and the forward's out (per-block partial rows, fixed-order
  *                 column sum: deterministic; the coordinate table is a constant buffer: no dcoords).
  * ------------------------------------------------------------------------------------ */

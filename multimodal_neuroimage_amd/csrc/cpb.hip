@@ -11,10 +11,9 @@
 namespace mmni {
 namespace cpb {
 
-constexpr int kMaxHeads = 32, kMaxHidden = 1024, kMaxNd = 3;
+constexpr int kMaxHeads = 32, kMaxHidden = 512, kMaxNd = 3;   // the reference's cpb_mlp is 512 wide
 constexpr int kEpb = 16;         // table entries per forward block
 constexpr int kBwdBlocks = 128;  // backward partial rows
-constexpr int kHpw = kMaxHeads / 4;   // heads per wave in the forward (4 waves)
 
 struct Args {
     int64_t tsz;
@@ -29,11 +28,15 @@ struct Args {
     float* part;           // backward: [block][heads * hidden | hidden * nd | hidden]
 };
 
-// hidden activations of kEpb entries in LDS; wave w owns heads w, w + 4, ...: their W2 rows are
-// loaded once into registers (every load in flight together), then each (entry, head) output is a
-// 64-lane dot over the hidden units with a butterfly sum (fixed order)
+// hidden activations of kEpb entries and the W2 rows in LDS (rows padded to an odd stride: the
+// reads below are conflict-free), then a thread per (entry, head) output sums its hidden units in
+// order (fixed order; no cross-lane reduction — a 64-lane butterfly per output was a chain of
+// ds_bpermute round trips)
+constexpr int kHs = kMaxHidden + 1;   // LDS row stride
 __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
-    __shared__ float h[kEpb][kMaxHidden];
+    extern __shared__ float fsm[];
+    float* h = fsm;                       // [kEpb][kHs]
+    float* w2s = fsm + kEpb * kHs;        // [heads][kHs]
     __shared__ float cs[kEpb][kMaxNd];
     const int64_t e0 = (int64_t)blockIdx.x * kEpb;
     const int ne = e0 + kEpb <= a.tsz ? kEpb : (int)(a.tsz - e0);
@@ -41,8 +44,11 @@ __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
         const int e = threadIdx.x / kMaxNd, d = threadIdx.x - e * kMaxNd;
         cs[e][d] = (e < ne && d < a.nd) ? a.coords[(e0 + e) * a.nd + d] : 0.f;
     }
-    // a thread per hidden unit (up to 4 units): its W1 row and bias in registers, the entries'
-    // coordinates from LDS — no global load inside the entry loop
+    for (int i = threadIdx.x; i < a.heads * a.hidden; i += 256) {
+        const int hd = i / a.hidden, j = i - hd * a.hidden;
+        w2s[hd * kHs + j] = a.w2[i];
+    }
+    // a thread per hidden unit (up to 4 units): its W1 row and bias in registers
     constexpr int UH = kMaxHidden / 256;
     float w1r[UH][kMaxNd], b1r[UH];
 #pragma unroll
@@ -62,36 +68,29 @@ __global__ __launch_bounds__(256) void cpb_fwd_kernel(Args a) {
             float z = b1r[u];
 #pragma unroll
             for (int d = 0; d < kMaxNd; ++d) z = fmaf(w1r[u][d], cs[e][d], z);
-            h[e][j] = fmaxf(z, 0.f);
-        }
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int JPL = kMaxHidden / 64;   // hidden units per lane (upper bound)
-    float w2r[kHpw][JPL];
-#pragma unroll
-    for (int u = 0; u < kHpw; ++u) {
-        const int hd = wave + 4 * u;
-#pragma unroll
-        for (int i = 0; i < JPL; ++i) {
-            const int j = lane + 64 * i;
-            w2r[u][i] = (hd < a.heads && j < a.hidden) ? a.w2[hd * a.hidden + j] : 0.f;
+            h[e * kHs + j] = fmaxf(z, 0.f);
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kHpw; ++u) {
-        const int hd = wave + 4 * u;
-        if (hd >= a.heads) break;   // wave-uniform
-        for (int e = 0; e < ne; ++e) {
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < JPL; ++i)
-                if (lane + 64 * i < a.hidden) s = fmaf(w2r[u][i], h[e][lane + 64 * i], s);
-            for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-            if (lane == 0) a.y[(e0 + e) * a.heads + hd] = 16.f / (1.f + expf(-s));
+    for (int o = threadIdx.x; o < ne * a.heads; o += 256) {
+        const int e = o / a.heads, hd = o - e * a.heads;
+        const float* hr = h + e * kHs;
+        const float* wr = w2s + hd * kHs;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four fixed-order partial chains
+        int j = 0;
+        for (; j + 3 < a.hidden; j += 4) {
+            s0 = fmaf(wr[j], hr[j], s0);
+            s1 = fmaf(wr[j + 1], hr[j + 1], s1);
+            s2 = fmaf(wr[j + 2], hr[j + 2], s2);
+            s3 = fmaf(wr[j + 3], hr[j + 3], s3);
         }
+        for (; j < a.hidden; ++j) s0 = fmaf(wr[j], hr[j], s0);
+        const float sv = (s0 + s1) + (s2 + s3);
+        a.y[(e0 + e) * a.heads + hd] = 16.f / (1.f + expf(-sv));
     }
 }
+
+size_t fwd_lds_bytes(int heads) { return (size_t)(kEpb + heads) * kHs * sizeof(float); }
 
 // a thread per hidden unit (hidden / 256 units each), a contiguous range of entries per block:
 // dz = dout * out * (1 - out / 16) (d(16 sigmoid)), dh_j = [h_j > 0] sum_h w2[h][j] dz_h, and the
@@ -194,7 +193,7 @@ using namespace mmni;
     MMNI_ARG_CHECK(tsz > 0 && nd >= 1 && nd <= cpb::kMaxNd && hidden >= 1 && hidden <= cpb::kMaxHidden &&     \
                        heads >= 1 && heads <= cpb::kMaxHeads,                                                  \
                    what ": tsz=%lld nd=%d hidden=%d heads=%d outside the supported range (nd <= 3, hidden <= " \
-                        "1024, heads <= 32)",                                                                  \
+                        "512, heads <= 32)",                                                                  \
                    (long long)tsz, nd, hidden, heads)
 
 extern "C" int mmni_cpb_fwd(int64_t tsz, int nd, int hidden, int heads, const float* coords, const float* w1,
@@ -205,7 +204,16 @@ extern "C" int mmni_cpb_fwd(int64_t tsz, int nd, int hidden, int heads, const fl
     a.tsz = tsz; a.nd = nd; a.hidden = hidden; a.heads = heads;
     a.coords = coords; a.w1 = w1; a.b1 = b1; a.w2 = w2; a.y = out;
     const unsigned blocks = (unsigned)((tsz + cpb::kEpb - 1) / cpb::kEpb);
-    cpb::cpb_fwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(a);
+    const size_t lds = cpb::fwd_lds_bytes(heads);   // <= 98.5 KB (32 heads x 512 hidden): raise the 64 KB cap
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cpb::cpb_fwd_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)cpb::fwd_lds_bytes(cpb::kMaxHeads));
+        if (e != hipSuccess) { set_error("cpb_fwd attribute: %s", hipGetErrorString(e)); return (int)e; }
+        attr_set = true;
+    }
+    cpb::cpb_fwd_kernel<<<blocks, 256, lds, (hipStream_t)stream>>>(a);
     return launch_status("cpb_fwd");
 }
 
@@ -227,12 +235,8 @@ extern "C" int mmni_cpb_bwd(int64_t tsz, int nd, int hidden, int heads, const fl
     const int blocks = cpb::bwd_blocks(tsz);
     hipStream_t s = (hipStream_t)stream;
     const int U = (hidden + 255) / 256;
-    switch (U) {
-        case 1: cpb::cpb_bwd_kernel<1><<<blocks, 256, 0, s>>>(a); break;
-        case 2: cpb::cpb_bwd_kernel<2><<<blocks, 256, 0, s>>>(a); break;
-        case 3: cpb::cpb_bwd_kernel<3><<<blocks, 256, 0, s>>>(a); break;
-        default: cpb::cpb_bwd_kernel<4><<<blocks, 256, 0, s>>>(a); break;
-    }
+    if (U == 1) cpb::cpb_bwd_kernel<1><<<blocks, 256, 0, s>>>(a);
+    else cpb::cpb_bwd_kernel<2><<<blocks, 256, 0, s>>>(a);
     int rc = launch_status("cpb_bwd");
     if (rc) return rc;
     ColSegs segs{};

@@ -149,6 +149,22 @@ __device__ __forceinline__ int key_end(const MhaArgs& a, int i) {
     return e < a.Tk ? e : a.Tk;
 }
 
+// XCD-aware block coordinates: workgroups are dealt to the 8 XCDs round-robin by linear id, so
+// with B*H a multiple of 8 the (tile, z) blocks of head bh are all placed on XCD bh % 8 (linear id
+// L: XCD L % 8, then the blocks of one bh in order) and its operand images stay in that XCD's L2.
+// Used from 32 row tiles up (T >= 2,048): at T = 4,096 it measured bwd 0.427 -> 0.367 ms (bf16,
+// E = 84), 0.52 -> 0.47 ms (fp32), fwd -8%; at T = 1,728 (27 tiles) the grid's own order was
+// ~10% faster (scripts/bench_mha.py, alternating A/B, r3i).  Otherwise the grid's coordinates.
+struct BlockXY { int x, y, z; };
+__device__ __forceinline__ BlockXY xcd_block() {
+    const int nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+    if (ny % 8 != 0 || nx < 32) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const int xcd = L & 7, j = L >> 3, per = nx * nz;
+    const int q = j / per, r = j - q * per;
+    return {r % nx, xcd + 8 * q, r / nx};
+}
+
 // block -> row tile: alternate the two ends of the sequence, so the causal mask's long and
 // short tiles interleave in dispatch order (even load per CU)
 __device__ __forceinline__ int zigzag(int x, int n) { return (x & 1) ? n - 1 - (x >> 1) : (x >> 1); }
@@ -495,9 +511,10 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     constexpr int SK = MT * G::XS, SV = G::ZR * G::ZS, STAGE = SK + SV;   // K ext + V Z
     constexpr int NBUF = Stages<STAGE * 2>::N;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * STAGE];
-    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+    const BlockXY blk = xcd_block();
+    const int bh = blk.y, b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int bx = a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x;
+    const int bx = a.causal > 0 ? zigzag(blk.x, a.nqt) : blk.x;
     const int q0 = bx * MT + wave * 16;
     const int qi = q0 + ln;
     const bool qok = qi < a.Tq;
@@ -612,14 +629,14 @@ struct DqLds {
     static constexpr int BYTES = NBUF * STAGE * 2;
 };
 template <int HDP, bool DROP, typename T>
-__device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int bx) {
+__device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int bx, int bh) {
     constexpr int TERMS = kTerms<T>;
     using G = Geo<HDP, TERMS>;
     using L = DqLds<HDP, TERMS>;
     constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
     constexpr int NBUF = L::NBUF;
     (void)SZ;
-    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+    const int b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
     const int q0 = bx * MT + wave * 16;
     const int qi = q0 + ln;
@@ -712,13 +729,13 @@ struct DkvLds {
     static constexpr int BYTES = NBUF * STAGE * 2;
 };
 template <int HDP, bool DROP, typename T>
-__device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, int bx) {
+__device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, int bx, int bh) {
     constexpr int TERMS = kTerms<T>;
     using G = Geo<HDP, TERMS>;
     using L = DkvLds<HDP, TERMS>;
     constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
     constexpr int NBUF = L::NBUF;
-    const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+    const int b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
     const int j0 = bx * MT + wave * 16;
     const int kj = j0 + ln;
@@ -846,12 +863,13 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
 template <int HDP, bool DROP, typename T>
 __global__ __launch_bounds__(256) void mha_bwd_mfma_kernel(MhaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t dyn_lds[];
-    if (blockIdx.z == 0) {
-        if ((int)blockIdx.x >= a.nqt) return;
-        mha_dq_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nqt) : (int)blockIdx.x);
+    const BlockXY blk = xcd_block();
+    if (blk.z == 0) {
+        if (blk.x >= a.nqt) return;
+        mha_dq_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blk.x, a.nqt) : blk.x, blk.y);
     } else {
-        if ((int)blockIdx.x >= a.nkt) return;
-        mha_dkv_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blockIdx.x, a.nkt) : (int)blockIdx.x);
+        if (blk.x >= a.nkt) return;
+        mha_dkv_body<HDP, DROP, T>(a, dyn_lds, a.causal > 0 ? zigzag(blk.x, a.nkt) : blk.x, blk.y);
     }
 }
 
