@@ -345,6 +345,9 @@ int mmni_fmri_band_split(const mmni_bandsplit_desc* d, const float* y, const int
  *   mmni_rowgemm_dw  dw[n][k] = sum_r dy[r][n] * x'[r][k], db[n] = sum_r dy[r][n] (db nullable);
  *                    x' = LayerNorm recomputed from the forward's mean / rstd when ln.  Row
  *                    chunks reduced in a fixed order: deterministic.  dy rows of stride ldy.
+ *   mmni_row_layernorm_fwd  y = LayerNorm(x) over rows of C <= 256 (+ mean, rstd for the backward):
+ *                    the crossmodal encoder's layer_norms / final LayerNorm on the per-op paths
+ *                    (crossmodal_transformer.py:145,159; the encoder's final norm :94).
  *   mmni_row_layernorm_bwd  dx = LayerNorm backward of dxn (+ dres), dgamma, dbeta over
  *                    rows of C <= 256 (fixed-order partial sums: deterministic).
  * All fp32.  Workspaces: mmni_rowgemm_dw_workspace_bytes / mmni_row_layernorm_bwd_workspace_bytes.
@@ -365,6 +368,8 @@ size_t mmni_rowgemm_dw_workspace_bytes(const mmni_rowgemm_desc* d);
 int mmni_rowgemm_dw(const mmni_rowgemm_desc* d, const float* x, const float* gamma, const float* beta,
                     const float* mean, const float* rstd, const float* dy, float* dw, float* db, void* workspace,
                     void* stream);
+int mmni_row_layernorm_fwd(int64_t rows, int C, const float* x, int64_t ldx, const float* gamma, const float* beta,
+                           float eps, float* y, int64_t ldy, float* mean, float* rstd, void* stream);
 size_t mmni_row_layernorm_bwd_workspace_bytes(int64_t rows, int C);
 int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
                            const float* gamma, const float* mean, const float* rstd, const float* dres,

@@ -75,6 +75,8 @@ SIGNATURES = {
     "mmni_rowgemm": (_c_int, [ctypes.POINTER(RowGemmDesc)] + [_vp] * 11),
     "mmni_rowgemm_dw_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RowGemmDesc)]),
     "mmni_rowgemm_dw": (_c_int, [ctypes.POINTER(RowGemmDesc)] + [_vp] * 10),
+    "mmni_row_layernorm_fwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _vp, ctypes.c_float, _vp, _c_i64, _vp, _vp,
+                                        _vp]),
     "mmni_row_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
     "mmni_cpb_fwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 6),
     "mmni_cpb_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int, _c_int, _c_int]),

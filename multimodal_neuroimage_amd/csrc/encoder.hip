@@ -548,6 +548,51 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
     }
 }
 
+// LayerNorm forward on rows of C <= 256: a wave per row, 4 columns per lane (two butterfly sums:
+// mean, then the centred second moment); (mean, rstd) written for the backward.
+__global__ __launch_bounds__(256) void row_ln_fwd_kernel(int64_t rows, int C, const float* __restrict__ x,
+                                                         int64_t ldx, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float* y,
+                                                         int64_t ldy, float* mean, float* rstd) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float gm[4], bt[4];
+    bool in[4];
+    const float* zp = g_zero4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j;
+        in[j] = c < C;
+        gm[j] = *(in[j] ? gamma + c : zp);
+        bt[j] = *(in[j] ? beta + c : zp);
+    }
+    const float invC = 1.0f / (float)C;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+        float v[4], s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = *(in[j] ? x + r * ldx + lane + 64 * j : zp);
+            s += v[j];
+        }
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const float mu = s * invC;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float d = in[j] ? v[j] - mu : 0.f;
+            q = fmaf(d, d, q);
+        }
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+        const float rs = 1.0f / sqrtf(q * invC + eps);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (in[j]) y[r * ldy + lane + 64 * j] = fmaf((v[j] - mu) * rs, gm[j], bt[j]);
+        if (lane == 0) {
+            mean[r] = mu;
+            rstd[r] = rs;
+        }
+    }
+}
+
 constexpr int kLnbBlocks = 768;   // ~2 rows per wave at 6,912 rows: a short dependent chain per wave
 
 // row chunks of a weight gradient: >= 64 rows each (4 groups per wave), at most 256, and a
@@ -713,4 +758,17 @@ extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int
                    "row_layernorm_bwd: leading dimensions below C");
     return enc_row_ln_bwd(rows, C, dxn, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma, dbeta,
                           workspace, (hipStream_t)stream);
+}
+
+extern "C" int mmni_row_layernorm_fwd(int64_t rows, int C, const float* x, int64_t ldx, const float* gamma,
+                                      const float* beta, float eps, float* y, int64_t ldy, float* mean, float* rstd,
+                                      void* stream) {
+    MMNI_ARG_CHECK(x && gamma && beta && y && mean && rstd, "row_layernorm_fwd: null pointer");
+    MMNI_ARG_CHECK(rows > 0 && C > 0 && C <= 256, "row_layernorm_fwd: C=%d outside 1..256", C);
+    MMNI_ARG_CHECK(ldx >= C && ldy >= C, "row_layernorm_fwd: leading dimensions below C");
+    int64_t blocks = (rows + 7) / 8;   // ~2 rows per wave
+    if (blocks > 4096) blocks = 4096;
+    enc::row_ln_fwd_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(rows, C, x, ldx, gamma, beta, eps, y,
+                                                                             ldy, mean, rstd);
+    return launch_status("row_layernorm_fwd");
 }

@@ -513,14 +513,46 @@ class _LayerNorm(torch.autograd.Function):
         return dx.view(ctx.shape), dgamma, dbeta, None
 
 
+class _RowLayerNorm(torch.autograd.Function):
+    """nn.LayerNorm over rows of C <= 256 (the crossmodal encoder's 84 / 168) on the wave-per-row
+    kernels (mmni_row_layernorm_fwd / _bwd).  Computes in fp32 and returns fp32 — what torch's
+    autocast does with layer_norm — from fp32 or bf16 input; the input gradient comes back in the
+    input's dtype."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).float().contiguous()
+        w, b = weight.float().contiguous(), bias.float().contiguous()
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        check(_lib.load().mmni_row_layernorm_fwd(rows, C, ptr(x2), C, ptr(w), ptr(b), float(eps), ptr(y), C,
+                                                 ptr(mean), ptr(rstd), stream_handle(x.device)),
+              "mmni_row_layernorm_fwd")
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.shape, ctx.dtype, ctx.wdtype = x.shape, x.dtype, weight.dtype
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        dx, dg, db = row_layernorm_bwd(dy.reshape(x2.shape).float().contiguous(), x2, w, mean, rstd)
+        return dx.view(ctx.shape).to(ctx.dtype), dg.to(ctx.wdtype), db.to(ctx.wdtype), None
+
+
 def layer_norm(x, ln):
-    """nn.LayerNorm `ln` applied to x (..., C) with the HIP kernels (C in 12/24/48/96); other widths
-    (the crossmodal stack's 84/168) stay on torch's ROCm LayerNorm.  No CPU path."""
+    """nn.LayerNorm `ln` applied to x (..., C) with the HIP kernels: the token kernels at C in
+    12/24/48/96, the wave-per-row kernels up to C = 256 (the crossmodal stack's 84/168), torch's
+    ROCm LayerNorm beyond.  No CPU path."""
     require_device(x, what="layer_norm")
     C = x.shape[-1]
-    if C not in LN_CHANNELS:
-        return ln(x)
-    return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
+    if C in LN_CHANNELS and x.dtype == torch.float32:
+        return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
+    if C <= 256 and ln.elementwise_affine and ln.bias is not None:
+        return _RowLayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
+    return ln(x)
 
 
 _DW_TILES = {(1, 1), (1, 2), (1, 3), (2, 1), (3, 1), (2, 2), (3, 3), (1, 4), (4, 1), (2, 3), (3, 2), (9, 3), (3, 9),

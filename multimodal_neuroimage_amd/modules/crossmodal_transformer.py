@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from .position_embedding import SinusoidalPositionalEmbedding
 from .multihead_attention import MultiheadAttention
-from ..functional import SplitKLinear, dropout_seed, encoder_layer_rows
+from ..functional import SplitKLinear, dropout_seed, encoder_layer_rows, layer_norm
 
 
 class TransformerEncoder(nn.Module):
@@ -57,7 +57,7 @@ class TransformerEncoder(nn.Module):
         for layer in self.layers:
             x = layer(x, x_k, x_v) if cross else layer(x)
         if self.normalize:
-            x = self.layer_norm(x)
+            x = layer_norm(x, self.layer_norm) if x.is_cuda else self.layer_norm(x)
         return x
 
     def max_positions(self):
@@ -123,7 +123,9 @@ class TransformerEncoderLayer(nn.Module):
 
     def maybe_layer_norm(self, i, x, before=False, after=False):
         assert before ^ after
-        return self.layer_norms[i](x) if after ^ self.normalize_before else x
+        if not (after ^ self.normalize_before):
+            return x
+        return layer_norm(x, self.layer_norms[i]) if x.is_cuda else self.layer_norms[i](x)
 
 
 def fill_with_neg_inf(t):

@@ -165,3 +165,28 @@ def test_fused_encoder_layer_matches_per_op_path(device, E, T, B, cross):
     worst = max(errs.items(), key=lambda kv: kv[1])
     print(f"fused encoder layer E={E} T={T} B={B} cross={cross}: worst {worst[0]} {worst[1]:.2e}")
     assert worst[1] < 1e-4, errs
+
+
+@pytest.mark.parametrize("rows,C,dtype", [(6912, 84, torch.float32), (32768, 168, torch.float32), (333, 84, torch.bfloat16),
+                                          (50, 200, torch.float32)])
+def test_row_layernorm_module_vs_fp64(device, rows, C, dtype):
+    """functional.layer_norm at the crossmodal widths (mmni_row_layernorm_fwd / _bwd): output and
+    every gradient against torch float64; fp32 output from bf16 input, as torch's autocast does."""
+    ln = torch.nn.LayerNorm(C).to(device)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.normal_()
+    g = torch.Generator(device=device).manual_seed(rows + C)
+    x = (torch.randn(rows, C, device=device, generator=g) * 2 + 1).to(dtype).requires_grad_(True)
+    gy = torch.randn(rows, C, device=device, generator=g)
+    y = MF.layer_norm(x, ln)
+    assert y.dtype == torch.float32
+    y.backward(gy)
+    xd = x.detach().double().requires_grad_(True)
+    wd, bd = ln.weight.detach().double().requires_grad_(True), ln.bias.detach().double().requires_grad_(True)
+    yd = torch.nn.functional.layer_norm(xd, (C,), wd, bd, ln.eps)
+    yd.backward(gy.double())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y, yd) < 1e-5
+    assert rel_err(x.grad.float(), xd.grad) < tol
+    assert rel_err(ln.weight.grad, wd.grad) < 1e-5 and rel_err(ln.bias.grad, bd.grad) < 1e-5
