@@ -546,7 +546,7 @@ def layer_norm(x, ln):
     """nn.LayerNorm `ln` applied to x (..., C) with the HIP kernels: the token kernels at C in
     12/24/48/96, the wave-per-row kernels up to C = 256 (the crossmodal stack's 84/168), torch's
     ROCm LayerNorm beyond.  No CPU path."""
-    require_device(x, what="layer_norm")
+    require_device(x, what="layer_norm", dtypes=(torch.float32, torch.bfloat16))
     C = x.shape[-1]
     if C in LN_CHANNELS and x.dtype == torch.float32:
         return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
