@@ -465,46 +465,32 @@ struct Stages {
     static constexpr int N = BYTES <= 20 * 1024 ? 2 : 1;
 };
 
-// the tile loop shared by the three kernels: load(t, slot) fills register slot `slot` (a
-// std::integral_constant: two register sets, statically indexed) from the images of tile t,
-// store(buf, slot) writes a slot to LDS stage buf, body(t, buf) computes on stage buf.
-// NBUF = 2: a tile's global loads are issued two tiles before its LDS store (a register set per
-// tile in flight), so each load has two tiles of compute to land; NBUF = 1: one set, load -> store
-// -> compute.
-using S0 = std::integral_constant<int, 0>;
-using S1 = std::integral_constant<int, 1>;
+// the tile loop shared by the three kernels: load(t) fills registers from the images of tile t,
+// store(buf) writes them to LDS stage buf, body(t, buf) computes on stage buf
 template <int NBUF, typename Load, typename Store, typename Body>
 __device__ __forceinline__ void tile_loop(int tb, int te, Load&& load, Store&& store, Body&& body) {
     if (tb >= te) return;
-    if constexpr (NBUF == 1) {
-        load(tb, S0{});
-        for (int t = tb; t < te; ++t) {
-            if (t > tb) __syncthreads();
-            store(0, S0{});
-            __syncthreads();
-            if (t + 1 < te) load(t + 1, S0{});
-            body(t, 0);
-        }
-    } else {
-        load(tb, S0{});
-        if (tb + 1 < te) load(tb + 1, S1{});
-        store(0, S0{});
-        if (tb + 2 < te) load(tb + 2, S0{});
+    load(tb);
+    if (NBUF == 2) {
+        store(0);
+        if (tb + 1 < te) load(tb + 1);
         __syncthreads();
-        // iteration of tile t with parity P = (t - tb) & 1 (slot / stage P^1 receive tile t + 1)
-        auto iter = [&](int t, auto P) {
-            constexpr int p = decltype(P)::value;
-            using Q = std::integral_constant<int, p ^ 1>;
-            body(t, p);
+    }
+    for (int t = tb; t < te; ++t) {
+        const int buf = NBUF == 2 ? (t - tb) & 1 : 0;
+        if (NBUF == 1) {
+            if (t > tb) __syncthreads();
+            store(0);
+            __syncthreads();
+            if (t + 1 < te) load(t + 1);
+        }
+        body(t, buf);
+        if (NBUF == 2) {
             if (t + 1 < te) {
-                store(p ^ 1, Q{});
-                if (t + 3 < te) load(t + 3, Q{});
+                store(buf ^ 1);
+                if (t + 2 < te) load(t + 2);
             }
             __syncthreads();
-        };
-        for (int t = tb; t < te; t += 2) {
-            iter(t, S0{});
-            if (t + 1 < te) iter(t + 1, S1{});
         }
     }
 }
@@ -544,21 +530,21 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vzg = a.vz + (int64_t)bh * a.nkt * G::ZT;
-    TileCopy<MT, G::EW> ck[2];
-    TileCopy<G::ZR, G::ZW> cv[2];
+    TileCopy<MT, G::EW> ck;
+    TileCopy<G::ZR, G::ZW> cv;
     mf4 o = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
     const int kend_blk = key_end(a, min(a.Tq - 1, bx * MT + MT - 1));
     const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 15)) : 0;
     tile_loop<NBUF>(
         0, (kend_blk + MT - 1) / MT,
-        [&](int t, auto S) {
-            ck[S].load(kxg + (int64_t)t * G::XT, tid);
-            cv[S].load(vzg + (int64_t)t * G::ZT, tid);
+        [&](int t) {
+            ck.load(kxg + (int64_t)t * G::XT, tid);
+            cv.load(vzg + (int64_t)t * G::ZT, tid);
         },
-        [&](int buf, auto S) {
-            ck[S].store(lds + buf * STAGE, tid);
-            cv[S].store(lds + buf * STAGE + SK, tid);
+        [&](int buf) {
+            ck.store(lds + buf * STAGE, tid);
+            cv.store(lds + buf * STAGE + SK, tid);
         },
         [&](int t, int buf) {
             const int k0 = t * MT;
@@ -673,8 +659,8 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vxg = a.vx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* kzg = a.kz + (int64_t)bh * a.nkt * G::ZT;
-    TileCopy<MT, G::EW> ck[2], cv[2];
-    TileCopy<G::ZR, G::ZW> cz[2];
+    TileCopy<MT, G::EW> ck, cv;
+    TileCopy<G::ZR, G::ZW> cz;
     const mf4 sinit = {-lse2, -lse2, -lse2, -lse2};
     const float di = DROP ? 0.f : -dl;
     const mf4 dinit = {di, di, di, di};
@@ -683,16 +669,16 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
     const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 15)) : 0;
     tile_loop<NBUF>(
         0, (kend_blk + MT - 1) / MT,
-        [&](int t, auto S) {
-            ck[S].load(kxg + (int64_t)t * G::XT, tid);
-            cv[S].load(vxg + (int64_t)t * G::XT, tid);
-            cz[S].load(kzg + (int64_t)t * G::ZT, tid);
+        [&](int t) {
+            ck.load(kxg + (int64_t)t * G::XT, tid);
+            cv.load(vxg + (int64_t)t * G::XT, tid);
+            cz.load(kzg + (int64_t)t * G::ZT, tid);
         },
-        [&](int buf, auto S) {
+        [&](int buf) {
             uint16_t* st = lds + buf * STAGE;
-            ck[S].store(st, tid);
-            cv[S].store(st + SX, tid);
-            cz[S].store(st + 2 * SX, tid);
+            ck.store(st, tid);
+            cv.store(st + SX, tid);
+            cz.store(st + 2 * SX, tid);
         },
         [&](int t, int buf) {
             const int k0 = t * MT;
@@ -770,9 +756,9 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
     const uint16_t* gxg = a.gx + (int64_t)bh * a.nqt * G::XT;
     const uint16_t* qzg = a.qz + (int64_t)bh * a.nqt * G::ZT;
     const uint16_t* gzg = a.gz + (int64_t)bh * a.nqt * G::ZT;
-    TileCopy<MT, G::EW> cq[2], cg[2];
-    TileCopy<G::ZR, G::ZW> czq[2], czg[2];
-    float pl[2] = {0.f, 0.f}, pd_[2] = {0.f, 0.f};   // the tile's -lse2 / -delta (threads < MT)
+    TileCopy<MT, G::EW> cq, cg;
+    TileCopy<G::ZR, G::ZW> czq, czg;
+    float pl = 0.f, pd_ = 0.f;   // the tile's -lse2 / -delta (threads < MT)
     mf4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
     // first query that can see the block's first key: j - i < diag  <=>  i > j - diag
     int i_begin = 0;
@@ -780,27 +766,27 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
     const int ib_w = a.causal > 0 ? max(0, j0 - a.causal + 1) : 0;   // this wave's first visible query
     tile_loop<NBUF>(
         i_begin / MT, a.nqt,
-        [&](int t, auto S) {
-            cq[S].load(qxg + (int64_t)t * G::XT, tid);
-            cg[S].load(gxg + (int64_t)t * G::XT, tid);
-            czq[S].load(qzg + (int64_t)t * G::ZT, tid);
-            czg[S].load(gzg + (int64_t)t * G::ZT, tid);
+        [&](int t) {
+            cq.load(qxg + (int64_t)t * G::XT, tid);
+            cg.load(gxg + (int64_t)t * G::XT, tid);
+            czq.load(qzg + (int64_t)t * G::ZT, tid);
+            czg.load(gzg + (int64_t)t * G::ZT, tid);
             if (tid < MT) {
                 const int i = t * MT + tid;
-                pl[S] = i < a.Tq ? -a.lse[(int64_t)bh * a.Tq + i] * kLog2e : -INFINITY;
-                pd_[S] = i < a.Tq ? -a.delta[(int64_t)bh * a.Tq + i] : 0.f;
+                pl = i < a.Tq ? -a.lse[(int64_t)bh * a.Tq + i] * kLog2e : -INFINITY;
+                pd_ = i < a.Tq ? -a.delta[(int64_t)bh * a.Tq + i] : 0.f;
             }
         },
-        [&](int buf, auto S) {
+        [&](int buf) {
             uint16_t* st = lds + buf * STAGE;
-            cq[S].store(st, tid);
-            cg[S].store(st + SX, tid);
-            czq[S].store(st + 2 * SX, tid);
-            czg[S].store(st + 2 * SX + SZ, tid);
+            cq.store(st, tid);
+            cg.store(st + SX, tid);
+            czq.store(st + 2 * SX, tid);
+            czg.store(st + 2 * SX + SZ, tid);
             float* f = reinterpret_cast<float*>(st + 2 * SX + 2 * SZ);
             if (tid < MT) {
-                f[tid] = pl[S];
-                f[MT + tid] = pd_[S];
+                f[tid] = pl;
+                f[MT + tid] = pd_;
             }
         },
         [&](int t, int buf) {
