@@ -7,11 +7,11 @@
 //                                   lock step, each key record an LDS broadcast read; online softmax;
 //                                   a 4-wave workgroup streams the query pairs of a list of windows
 //                                   (all lanes busy)
-//   backward  wattn_bwd_q4m_kernel  lane = query quad (y + 3, z + 3 partners); the wave walks the
-//                                   54 key quads; per step p and ds of 16 (query, key) pairs give
-//                                   dq (registers), the bias-table gradient (private LDS image) and
-//                                   dk / dv partials that a 64-lane butterfly reduces to the final
-//                                   sums of the step's 4 keys -- one pass, no recomputation
+//   backward  wattn_bwd_q4k_kernel  lane = key quad (y + 3, z + 3 partners); the wave walks the
+//                                   54 query quads; per step p and ds of 16 (query, key) pairs give
+//                                   dk / dv (registers), the bias-table gradient (private LDS image)
+//                                   and dq partials that a 64-lane butterfly reduces to the final
+//                                   sums of the step's 4 queries -- one pass, no recomputation
 //
 // LDS facts that shape them (measured here, gfx950): a broadcast record is read 16 bytes at a time
 // from a 16-byte-aligned address (ds_read_b128: 4 LDS cycles; the compiler's ds_read2_b64 pairs take
@@ -19,8 +19,8 @@
 // coordinates and codes are scalar loop counters, and every table access of a step is one address
 // register plus immediate offsets.
 //
-// Bias-table gradient without atomics.  At one step the wave's lanes hold distinct queries against
-// the same keys, so the relative-position entries they update, code(q) - code(k) + off, are
+// Bias-table gradient without atomics.  At one step the wave's lanes hold distinct keys against
+// the same queries, so the relative-position entries they update, code(q) - code(k) + off, are
 // pairwise distinct.  Each wave therefore read-modify-writes its OWN fp32 copy of the table in LDS
 // with plain loads and stores: no atomics, no fixed-point scale, no max|dO| pre-pass (LDS float
 // atomics measured ~8x slower).  A workgroup always serves the same head pair; its waves' copies
@@ -247,28 +247,21 @@ __device__ __forceinline__ void fwd_loop(const Row (&q)[2], f2 (&m)[2], f2 (&l)[
 }
 
 // ------------------------------------------------------------------------------------
-// "quad" layout of 6^3 windows: a lane owns the row quad {b, b + 18, b + 108, b + 126} (its
-// (y + 3, z + 3) partners), b = (z', y', x) with z', y' < 3: 54 lanes = one wave per (window, head
-// pair).  The wave walks the 54 key quads in lock step, so each broadcast record (4 keys x k, v)
-// feeds 16 (query, key) pairs instead of 4, and the 16 pairs of a step touch only 9 table entries
+// "quad" layout of 6^3 windows: the row quad {b, b + 18, b + 108, b + 126} (the (y + 3, z + 3)
+// partners of b = (z', y', x), z', y' < 3): 54 quads per window, one lane each, one wave per (window,
+// head pair).  The wave walks the other side's 54 quads in lock step, so each broadcast record feeds
+// 16 (query, key) pairs instead of 4, and the 16 pairs of a step touch only 9 table entries
 // (relative offsets a * 3 TW + b * 3 TH, a, b in {-1, 0, 1}).  The bases' codes hit each of the 32
 // 8-byte bank pairs once in lanes 0-31 and at most once in lanes 32-53 (kPermQ), so every
 // per-lane table access is conflict-free.  The 9 x 54 entries of one step are pairwise distinct
-// (codes of bases differ by less than 3 in every digit), so the private table read-modify-write
-// of a step never aliases across lanes.
+// (codes of bases differ by less than 3 in every digit, the slot offsets by multiples of 3), so the
+// private table read-modify-write of a step never aliases across lanes.
 // ------------------------------------------------------------------------------------
 namespace q4 {
 constexpr int NB = 54;                              // row quads per window
 constexpr int TW = 121, TH = 11, OFF = 665, TSZ = 1331;
 constexpr int EB = 8;                               // table entry: f2 over the head pair
-constexpr int DMIN = 3 * TW + 3 * TH + 5;           // 401: entry offsets D + DMIN - x are >= 0
-constexpr int REC = 128;                            // key-quad record: 4 keys x (k f4, v f4)
-constexpr int KVB = NB * REC;                       // 6912 B of records per wave
 constexpr int WAVES = 4;                            // waves per workgroup (one head pair per workgroup)
-constexpr int TABB = TSZ * EB;                      // 10648 B per table image
-constexpr int TAB = WAVES * KVB;                    // bias table offset (records first: row bases >= 0)
-constexpr int DT = (TAB + TABB + 15) & ~15;         // gradient images, one per wave
-constexpr int LDS_A = DT + WAVES * TABB;            // 80896 B: two workgroups per CU
 __constant__ unsigned char kPermQ[NB] = {0,  1,  2,  3,  4,  5,  26, 27, 28, 29, 50, 6,  7,  8,  9,  10, 11, 32,
                                          33, 34, 35, 39, 12, 13, 14, 15, 16, 17, 21, 22, 23, 44, 18, 19, 20, 24,
                                          25, 30, 31, 36, 37, 38, 40, 41, 42, 43, 45, 46, 47, 48, 49, 51, 52, 53};
@@ -296,18 +289,10 @@ __device__ __forceinline__ Work work(int NHG, int wave) {
 }
 }  // namespace q4
 
-// ------------------------------------------------------------------------------------
-// merged backward, quad layout: pass A's walk (lane = query quad, key quads broadcast) also forms
-// the key side.  Per step a lane holds, for the 4 keys of the quad, its partial dk and dv over its
-// 4 query rows: 32 floats = 16 f2 over the head pair, value i = kind * 16 + v * 4 + c * 2 + h
-// (kind 0 dk, 1 dv; key v, dim c, head h).  A fixed butterfly over the 64 lanes (v_permlane32_swap,
-// v_permlane16_swap, then DPP row_ror:8 / row_half_mirror / quad xor 2 / xor 1) leaves lane l with
-// the full sum of value l >> 1, which lane l (even) stores.  Every key quad is visited once per
-// window, so those sums are final: no dk/dv accumulation, and p, ds are formed once per (query,
-// key) instead of once in each pass.  Deterministic (fixed lane tree, fixed row order).
-// ------------------------------------------------------------------------------------
+// 64-lane butterfly helpers of the merged backward's reductions: v_permlane32_swap /
+// v_permlane16_swap exchange register halves across lane halves (one instruction per register
+// pair), DPP forms x + partner(x) within a row (scripts/check_permlane.hip checks the semantics).
 namespace q4 {
-
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
@@ -322,244 +307,318 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
     a = __uint_as_float(r[0]);
     b = __uint_as_float(r[1]);
 }
-
-// 16 f2 partials per lane -> lane l returns the 64-lane sum of value l >> 1.  Stages 1-2 swap
-// register halves across lane halves (v_permlane32_swap / v_permlane16_swap: one instruction per
-// register pair).  Stages 3-6 pair lanes l and l ^ d inside a row; there every lane forms BOTH
-// candidate sums with the DPP operand folded into v_add_f32 (x + dpp(x), one instruction each) and
-// keeps the one its lane bit selects -- 3 instructions per output float instead of two selects, a
-// zero-initialised v_mov_b32_dpp and half a packed add.  The operand order (own value first,
-// partner's second) is that of the keep/send formulation, so the sums are bitwise the same.
-__device__ __forceinline__ float reduce32(f2 (&P)[16], int lane) {
-    f2 R[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {   // lanes 0-31 keep f2 k (dk), lanes 32-63 f2 k + 8 (dv)
-        float a0 = P[k].x, b0 = P[k + 8].x, a1 = P[k].y, b1 = P[k + 8].y;
-        swap32(a0, b0);
-        swap32(a1, b1);
-        R[k] = (f2){a0, a1} + (f2){b0, b1};
-    }
-    f2 S[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // rows 0, 2 keep k (keys 0, 1), rows 1, 3 keep k + 4 (keys 2, 3)
-        float a0 = R[k].x, b0 = R[k + 4].x, a1 = R[k].y, b1 = R[k + 4].y;
-        swap16(a0, b0);
-        swap16(a1, b1);
-        S[k] = (f2){a0, a1} + (f2){b0, b1};
-    }
-    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
-    // lane bit 3: key 0 or 1 of the pair (row_ror:8 partner = lane ^ 8)
-    float T[4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const float lo_x = S[k].x + dpp<0x128>(S[k].x), hi_x = S[k + 2].x + dpp<0x128>(S[k + 2].x);
-        const float lo_y = S[k].y + dpp<0x128>(S[k].y), hi_y = S[k + 2].y + dpp<0x128>(S[k + 2].y);
-        T[2 * k] = b3 ? hi_x : lo_x;
-        T[2 * k + 1] = b3 ? hi_y : lo_y;
-    }
-    // lane bit 2: dim c (row_half_mirror partner = lane ^ 7 within 8)
-    const float u0 = T[0] + dpp<0x141>(T[0]), u2 = T[2] + dpp<0x141>(T[2]);
-    const float u1 = T[1] + dpp<0x141>(T[1]), u3 = T[3] + dpp<0x141>(T[3]);
-    const float Ux = b2 ? u2 : u0, Uy = b2 ? u3 : u1;
-    // lane bit 1: head h (quad partner lane ^ 2), then lane ^ 1
-    const float vx = Ux + dpp<0x4E>(Ux), vy = Uy + dpp<0x4E>(Uy);
-    const float V = b1 ? vy : vx;
-    return V + dpp<0xB1>(V);
-}
 }  // namespace q4
 
-// a zero f2 in one 64-bit move: the spare lanes' partials (the compiler splits a plain f2 zero
-// into two 32-bit moves, 32 per step)
-__device__ __forceinline__ f2 zero2() {
-    double r;
-    asm volatile("v_mov_b64 %0, 0" : "=v"(r));
-    return __builtin_bit_cast(f2, r);
-}
+// ------------------------------------------------------------------------------------
+// key-stationary merged backward (the C3 kernel).  A lane owns the KEY quad {b, b + 18, b + 108,
+// b + 126} (k, v and the dk, dv accumulators stay in its registers for the whole window) and the
+// wave walks the 54 QUERY quads, each a broadcast record of 4 rows x (q * scale * log2 e, dO) plus
+// -delta and lse.  Per step a lane forms p and ds of its 16 (query, key) pairs once; dk and dv
+// accumulate in place, and only dq -- 4 rows x 2 dims x 2 heads = 16 floats -- needs the 64-lane
+// sum (reduce16), whose results replace the step's dead record.  (The query-stationary walk of
+// r2g-r3f held dq in registers and reduced the step's 32 dk / dv values instead: 24 lane-swap
+// instructions per step against 12 here, 343 instructions per step against 308.)  The bias-table
+// entries of a step are code(q) - code(k) + off with the lane's key code negated: kPermQ still
+// spreads them over the 32 bank pairs, and they stay pairwise distinct, so the private table
+// image is still updated with plain loads and stores.
+//
+// LDS: the query records (192 B per quad) do not fit next to four table images for the whole
+// window, so each wave walks the window in two halves -- quad rows 0-4 (30 quads) and 5-8 (24) --
+// through one 30-record ring: the owners of a half's quads stage its records, the wave walks it,
+// the owners write their dq rows out of the ring, and the next half is staged in its place.  The
+// fold of 2^-lse into dO and -delta is decided per half.  (Measured and dropped: loading the
+// second half's rows by LDS-DMA into the dead slots during the first half's last row; the spills
+// it forced cost more than the hidden latency, r3m: 2.73 against 2.52 ms.)
+// ------------------------------------------------------------------------------------
+namespace k4 {
+constexpr int REC = 192;                            // q~ f4 + dO f4 per row (128 B) | -delta f2 x 4 | lse2 f2 x 4
+constexpr int HALF_ROWS = 5;                        // quad rows (6 quads each) of the first half
+constexpr int RING = HALF_ROWS * 6 * REC;           // 5760 B per wave
+constexpr int WAVES = 4;
+constexpr int TABB = q4::TSZ * q4::EB;              // 10648 B per table image
+constexpr int TAB = WAVES * RING;                   // bias table after the rings
+constexpr int DT = (TAB + TABB + 15) & ~15;         // gradient images, one per wave
+constexpr int LDS = DT + WAVES * TABB;              // 76288 B: two workgroups per CU
+constexpr int DMN = 3 * q4::TW + 3 * q4::TH;        // 396: slot offsets dcode(e) + DMN >= 0
+static_assert(q4::OFF - (2 * q4::TW + 2 * q4::TH + 5) - DMN >= 0, "lane table bases must be >= 0");
 
+// 8 f2 dq partials per lane, value i = (u, c, h) in P[u * 2 + c].{x: h0, y: h1} -> lane l returns
+// the 64-lane sum of value (u = l >> 4 & 3, c = l >> 3 & 1, h = l >> 2 & 1).  Stages 1-2 swap
+// register halves across lane halves; stages 3-4 form BOTH candidate sums x + dpp(x) and keep the
+// one the lane bit selects; 5-6 add the quad partners.  Fixed lane tree: bitwise deterministic.
+__device__ __forceinline__ float reduce16(f2 (&P)[8], int lane) {
+    f2 R[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // lanes 0-31 keep rows u = 0, 1; lanes 32-63 rows 2, 3
+        float a0 = P[k].x, b0 = P[k + 4].x, a1 = P[k].y, b1 = P[k + 4].y;
+        q4::swap32(a0, b0);
+        q4::swap32(a1, b1);
+        R[k] = (f2){a0, a1} + (f2){b0, b1};
+    }
+    f2 S[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // rows 0, 2 of 16 lanes keep u & 1 = 0, rows 1, 3 keep u & 1 = 1
+        float a0 = R[k].x, b0 = R[k + 2].x, a1 = R[k].y, b1 = R[k + 2].y;
+        q4::swap16(a0, b0);
+        q4::swap16(a1, b1);
+        S[k] = (f2){a0, a1} + (f2){b0, b1};
+    }
+    const bool b3 = lane & 8, b2 = lane & 4;
+    // lane bit 3: dim c (row_ror:8 partner = lane ^ 8)
+    const float lo_x = S[0].x + q4::dpp<0x128>(S[0].x), hi_x = S[1].x + q4::dpp<0x128>(S[1].x);
+    const float lo_y = S[0].y + q4::dpp<0x128>(S[0].y), hi_y = S[1].y + q4::dpp<0x128>(S[1].y);
+    const float Tx = b3 ? hi_x : lo_x, Ty = b3 ? hi_y : lo_y;
+    // lane bit 2: head h (row_half_mirror partner = lane ^ 7 within 8), then quad xor 2 and xor 1
+    const float ux = Tx + q4::dpp<0x141>(Tx), uy = Ty + q4::dpp<0x141>(Ty);
+    const float U = b2 ? uy : ux;
+    const float V = U + q4::dpp<0x4E>(U);
+    return V + q4::dpp<0xB1>(V);
+}
+}  // namespace k4
+
+// walk of the query-quad rows [r0, r1), whose records start at ring offset recw (row r0)
 template <bool MASKED, bool FOLD>
-__device__ __forceinline__ void q4M_loop(const Row (&q)[4], const Row (&dO)[4], const f2 (&lse2)[4],
-                                         const f2 (&ndl)[4], Row (&dq)[4], int lcode, const int (&rq)[4],
-                                         const bc::Regions& reg, char* sm, int kvw, int dtw, bool lane_ok) {
+__device__ __forceinline__ void q4k_walk(int r0, int r1, const Row (&kk)[4], const Row (&vv)[4], Row (&dk)[4],
+                                         Row (&dv)[4], const int (&rk)[4], const bc::Regions& reg, char* sm,
+                                         int recw, int dtw, uint32_t lane_e, f2 live) {
     using namespace q4;
     const int lane = threadIdx.x & 63;
-    char* kv = sm + kvw;
-    const uint32_t lane_e = (uint32_t)((lcode + OFF - DMIN) * EB);
-    // where this lane's key-side sum (value l >> 1 = kind, key v, dim c, head h) goes: the step's
-    // key-quad record, dead once the step has read it, as [v][kind][h c] (the rows' natural order)
-    const int soff = ((lane >> 3) & 3) * 32 + (lane >> 5) * 16 + ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4;
+    // where this lane's dq sum (u, c, h) goes in the step's dead record: [u][h c], the row order
+    const int soff = ((lane >> 4) & 3) * 16 + ((lane >> 2) & 1) * 8 + ((lane >> 3) & 1) * 4;
     // The table image offset goes through an empty asm after each step's stores, so the compiler
     // treats the next step's table reads as possibly aliasing them (other lanes' entries) and keeps
-    // them behind the stores; LDS executes a wave's accesses in order, so no wait is needed.  (Issuing
-    // the next step's records before the lane reduction measured no faster.)
-    f2 kk[4][2], vv[4][2], bt[9], od[9];
-    auto load = [&](const char* rec, const char* te) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32), kk[v][0], kk[v][1]);
-            bc::ld_pair(reinterpret_cast<const f2*>(rec + v * 32 + 16), vv[v][0], vv[v][1]);
-        }
-#pragma unroll
-        for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(te + (dcode(e) + DMIN) * EB);
-    };
+    // them behind the stores; LDS executes a wave's accesses in order, so no wait is needed.
     int dto = dtw;   // this wave's table-gradient image (an LDS offset: the accesses stay ds_*)
-    for (int zr = 0; zr < 3; ++zr) {
-        for (int yr = 0; yr < 3; ++yr) {
-            const uint32_t trow = lane_e - (uint32_t)((zr * TW + yr * TH) * EB);
-            const char* kvr = kv + (zr * 3 + yr) * 6 * REC;
+    for (int r = r0; r < r1; ++r) {
+        const int zr = r / 3, yr = r - 3 * (r / 3);
+        const uint32_t trow = lane_e + (uint32_t)((zr * TW + yr * TH) * EB);
+        char* rrow = sm + recw + (r - r0) * 6 * k4::REC;
 #pragma unroll
-            for (int x = 0; x < 6; ++x) {
-                // spare lanes skip the step and contribute zero partials (as straight-line code for
-                // all lanes, with zero rows, the compiler spilled ~800 VGPRs; the branch does not)
-                f2 P[16];
+        for (int x = 0; x < 6; ++x) {
+            f2 P[8];
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                char* dp = sm + dto + trow;
+                const char* tp = sm + k4::TAB + trow;
+                const char* rec = rrow + x * k4::REC;
+                f2 od[9], bt[9];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) P[i] = zero2();
-                if (lane_ok) {
-                    char* dp = sm + dto + trow;
-                    // this step's table-gradient entries (after the previous step's stores: see dto)
+                for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (x + dcode(e) + k4::DMN) * EB);
+                Row qs[4], dO[4];
+                f2 nd[4], ls[4];
 #pragma unroll
-                    for (int e = 0; e < 9; ++e) od[e] = *reinterpret_cast<const f2*>(dp + (dcode(e) + DMIN - x) * EB);
-                    load(kvr + x * REC, sm + TAB + trow - x * EB);
-                    int rk[4] = {0, 0, 0, 0};
-                    if (MASKED) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) rk[v] = bc::region_code(reg, zr + 3 * (v >> 1), yr + 3 * (v & 1), x);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            const int e = slot(u, v);
-                            f2 base = FOLD ? bt[e] : bt[e] - lse2[u];
-                            if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
-                            f2 s = bc::pfma(q[u].x[0], kk[v][0], base);
-                            s = bc::pfma(q[u].x[1], kk[v][1], s);
-                            const f2 p = bc::exp2_2(s);
-                            f2 tt = bc::pfma(dO[u].x[0], vv[v][0], ndl[u]);
-                            tt = bc::pfma(dO[u].x[1], vv[v][1], tt);
-                            const f2 ds = p * tt;
-                            dq[u].x[0] = bc::pfma(ds, kk[v][0], dq[u].x[0]);
-                            dq[u].x[1] = bc::pfma(ds, kk[v][1], dq[u].x[1]);
-                            od[e] += ds;
-                            if (u == 0) {   // first row: plain products (P is zero)
-                                P[v * 2] = ds * q[0].x[0];              // dk, dim 0
-                                P[v * 2 + 1] = ds * q[0].x[1];          // dk, dim 1
-                                P[8 + v * 2] = p * dO[0].x[0];          // dv, dim 0
-                                P[8 + v * 2 + 1] = p * dO[0].x[1];      // dv, dim 1
-                            } else {
-                                P[v * 2] = bc::pfma(ds, q[u].x[0], P[v * 2]);
-                                P[v * 2 + 1] = bc::pfma(ds, q[u].x[1], P[v * 2 + 1]);
-                                P[8 + v * 2] = bc::pfma(p, dO[u].x[0], P[8 + v * 2]);
-                                P[8 + v * 2 + 1] = bc::pfma(p, dO[u].x[1], P[8 + v * 2 + 1]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (dcode(e) + DMIN - x) * EB) = od[e];
+                for (int u = 0; u < 4; ++u) {
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 32), qs[u].x[0], qs[u].x[1]);
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + u * 32 + 16), dO[u].x[0], dO[u].x[1]);
                 }
-                asm volatile("" : "+v"(dto));   // next reads: behind the stores above (see the top)
-                // all 64 lanes take part in the reduction (spare lanes contribute zeros)
-                const float sum = reduce32(P, lane);
-                // the final sums of key quad n = (zr, yr, x) replace its record (read above: LDS
-                // runs a wave's accesses in order); the owner lane writes the rows out after the walk
-                if ((lane & 1) == 0) *reinterpret_cast<float*>(kv + ((zr * 3 + yr) * 6 + x) * REC + soff) = sum;
-                __builtin_amdgcn_sched_barrier(0);
+                bc::ld_pair(reinterpret_cast<const f2*>(rec + 128), nd[0], nd[1]);
+                bc::ld_pair(reinterpret_cast<const f2*>(rec + 144), nd[2], nd[3]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nd[u] *= live;   // spare lanes: ds = p * 0 = 0
+                if (!FOLD) {
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + 160), ls[0], ls[1]);
+                    bc::ld_pair(reinterpret_cast<const f2*>(rec + 176), ls[2], ls[3]);
+                }
+#pragma unroll
+                for (int e = 0; e < 9; ++e) bt[e] = *reinterpret_cast<const f2*>(tp + (x + dcode(e) + k4::DMN) * EB);
+                int rq[4] = {0, 0, 0, 0};
+                if (MASKED) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) rq[u] = bc::region_code(reg, zr + 3 * (u >> 1), yr + 3 * (u & 1), x);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int e = slot(u, v);
+                        f2 base = FOLD ? bt[e] : bt[e] - ls[u];
+                        if (MASKED) base += bc::splat(rk[v] == rq[u] ? 0.f : kMask2);
+                        f2 s = bc::pfma(qs[u].x[0], kk[v].x[0], base);
+                        s = bc::pfma(qs[u].x[1], kk[v].x[1], s);
+                        const f2 p = bc::exp2_2(s);
+                        f2 tt = bc::pfma(dO[u].x[0], vv[v].x[0], nd[u]);
+                        tt = bc::pfma(dO[u].x[1], vv[v].x[1], tt);
+                        const f2 ds = p * tt;
+                        if (v == 0) {   // first key: plain products (P is zero)
+                            P[u * 2] = ds * kk[0].x[0];
+                            P[u * 2 + 1] = ds * kk[0].x[1];
+                        } else {
+                            P[u * 2] = bc::pfma(ds, kk[v].x[0], P[u * 2]);
+                            P[u * 2 + 1] = bc::pfma(ds, kk[v].x[1], P[u * 2 + 1]);
+                        }
+                        dk[v].x[0] = bc::pfma(ds, qs[u].x[0], dk[v].x[0]);
+                        dk[v].x[1] = bc::pfma(ds, qs[u].x[1], dk[v].x[1]);
+                        dv[v].x[0] = bc::pfma(p, dO[u].x[0], dv[v].x[0]);
+                        dv[v].x[1] = bc::pfma(p, dO[u].x[1], dv[v].x[1]);
+                        od[e] += ds;
+                    }
+                    // pin the accumulators here: without it the compiler defers the dk / dv
+                    // updates past the step (holding every p and ds: spilled)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        asm volatile("" : "+v"(dk[v].x[0]), "+v"(dk[v].x[1]), "+v"(dv[v].x[0]), "+v"(dv[v].x[1]));
+                }
+#pragma unroll
+                for (int e = 0; e < 9; ++e) *reinterpret_cast<f2*>(dp + (x + dcode(e) + k4::DMN) * EB) = od[e];
             }
+            asm volatile("" : "+v"(dto));   // next reads: behind the stores above (see dto)
+            const float sum = k4::reduce16(P, lane);
+            // the final dq sums of query quad (r, x) replace its record (read above: LDS runs a
+            // wave's accesses in order); the owner lane writes the rows out after the half
+            if ((lane & 3) == 0) *reinterpret_cast<float*>(rrow + x * k4::REC + soff) = sum;
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
 
-// merged backward: dq, dk, dv and the table gradient in one walk (4 waves per workgroup as pass A)
-__global__ __launch_bounds__(q4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
-void wattn_bwd_q4m_kernel(WAArgs a, float* part) {
+// stage the query records of a half into the wave's ring; returns the fold flag of the half (every
+// row of the half has |lse| <= kFoldMax in the log2 domain)
+__device__ __forceinline__ bool q4k_stage(const WAArgs& a, bool mine, int slot_off, const int64_t (&row)[4], int coff,
+                                          int hp, int NHT, f2 qscale) {
+    Row qs[4], dO[4];
+    f2 nd[4], ls[4];
+    bool ok = true;
+    if (mine) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            // opaque row copies: otherwise the compiler forms every row's q / dO / o / lse / dq
+            // address once per window, keeps them across both walks and spills them (reloaded here
+            // at memory latency)
+            int64_t rw = row[u];
+            asm volatile("" : "+v"(rw));
+            qs[u] = bc::load_row_pk(a.q + rw * a.qs + coff);
+            dO[u] = bc::load_row_pk(a.dout + rw * a.os + coff);
+            const Row o = bc::load_row_pk(a.o + rw * a.os + coff);
+            qs[u].x[0] *= qscale;
+            qs[u].x[1] *= qscale;
+            nd[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
+            ls[u] = (f2){a.lse[rw * NHT + 2 * hp], a.lse[rw * NHT + 2 * hp + 1]} * kLog2e;
+            ok = ok && bc::fold_ok(ls[u]);
+        }
+    }
+    const bool fold = __all(ok);   // lanes outside the half vote true
+    if (mine) {
+        extern __shared__ __attribute__((aligned(16))) float smem[];
+        char* rec = reinterpret_cast<char*>(smem) + slot_off;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (fold) {
+                const f2 e = bc::exp2_2(-ls[u]);
+                dO[u].x[0] *= e;
+                dO[u].x[1] *= e;
+                nd[u] *= e;
+            }
+            *reinterpret_cast<bc::f4*>(rec + u * 32) = (bc::f4){qs[u].x[0].x, qs[u].x[0].y, qs[u].x[1].x, qs[u].x[1].y};
+            *reinterpret_cast<bc::f4*>(rec + u * 32 + 16) =
+                (bc::f4){dO[u].x[0].x, dO[u].x[0].y, dO[u].x[1].x, dO[u].x[1].y};
+        }
+        *reinterpret_cast<bc::f4*>(rec + 128) = (bc::f4){nd[0].x, nd[0].y, nd[1].x, nd[1].y};
+        *reinterpret_cast<bc::f4*>(rec + 144) = (bc::f4){nd[2].x, nd[2].y, nd[3].x, nd[3].y};
+        *reinterpret_cast<bc::f4*>(rec + 160) = (bc::f4){ls[0].x, ls[0].y, ls[1].x, ls[1].y};
+        *reinterpret_cast<bc::f4*>(rec + 176) = (bc::f4){ls[2].x, ls[2].y, ls[3].x, ls[3].y};
+    }
+    asm volatile("" ::: "memory");   // the records are written before the walk reads them
+    return fold;
+}
+
+// dq rows of a half's quads from their ring slots (the walk left the sums there)
+__device__ __forceinline__ void q4k_flush(const WAArgs& a, bool mine, const char* rec, const int64_t (&row)[4],
+                                          int coff) {
+    if (mine) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            int64_t rw = row[u];
+            asm volatile("" : "+v"(rw));   // as in q4k_stage
+            const bc::f4 d = *reinterpret_cast<const bc::f4*>(rec + u * 16);
+            *reinterpret_cast<bc::f4*>(a.dq + rw * a.qs + coff) = d * a.scale;
+        }
+    }
+    asm volatile("" ::: "memory");   // the next half's records stay behind these reads
+}
+
+__global__ __launch_bounds__(k4::WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void wattn_bwd_q4k_kernel(WAArgs a, float* part) {
     using namespace q4;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     char* sm = reinterpret_cast<char*>(smem);
     const WGeom& g = a.g;
     const int NHG = a.hsplit, NHT = 2 * NHG;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = tid >> 6;
     const Work wk = work(NHG, wave);
-    float* tab = reinterpret_cast<float*>(sm + TAB);
+    float* tab = reinterpret_cast<float*>(sm + k4::TAB);
     for (int e = tid; e < TSZ * 2; e += blockDim.x) tab[e] = a.table[(e >> 1) * NHT + 2 * wk.hp + (e & 1)] * kLog2e;
-    float* dtf = reinterpret_cast<float*>(sm + DT);
-    for (int e = tid; e < WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
+    float* dtf = reinterpret_cast<float*>(sm + k4::DT);
+    for (int e = tid; e < k4::WAVES * TSZ * 2; e += blockDim.x) dtf[e] = 0.f;
     __syncthreads();
+    // Spare lanes (54..63) run every step with k = v = 0 and -delta masked to 0, so their ds and dq
+    // partials are exact zeros and their table-image updates add zero.  They share the virtual key
+    // code kSpareCode: its entries code(q) - kSpareCode + off + dcode(e) never meet a real lane's at
+    // the same step (kSpareCode - code(b) + dcode(e) - dcode(e') has a units digit 10 - x of 5..10,
+    // never a multiple of 11, while the slot offsets are) and stay inside the image (259..1320).
+    constexpr int kSpareCode = 10;
     const bool lane_ok = lane < NB;
-    const int beta = lane_ok ? (int)kPermQ[lane] : 0;   // spare lanes (54..63) only join the reductions
-    const int tb0 = base_token(beta), lcode = base_code(beta);
-    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6;
-    const int kvw = wave * KVB, dtw = DT + wave * TABB;
+    const int beta = lane_ok ? (int)kPermQ[lane] : 0;
+    const int tb0 = base_token(beta);
+    const int bz = beta / 18, by = (beta / 6) % 3, bx = beta % 6, brow = beta / 6;
+    const uint32_t lane_e = (uint32_t)((OFF - (lane_ok ? base_code(beta) : kSpareCode) - k4::DMN) * EB);
+    const f2 live = bc::splat(lane_ok ? 1.f : 0.f);
+    const int recw = wave * k4::RING, dtw = k4::DT + wave * k4::TABB;
     const int coff = wk.hp * 4;
     const f2 qscale = bc::splat(a.scale * kLog2e);
     for (int j = wk.j0;; j += wk.dj) {
         const int w = wk.xcd + 8 * j;
         if (w >= g.nwin) break;
-        Row q[4], dO[4], dq[4];
-        f2 lse2[4], ndl[4];
-        int rq[4] = {0, 0, 0, 0};
-        int64_t rowk[4] = {0, 0, 0, 0};
         const bc::Regions reg = bc::window_regions(g, w);
+        Row kk[4], vv[4], dk[4], dv[4];
+        int rk[4] = {0, 0, 0, 0};
+        int64_t row[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            q[u].x[0] = q[u].x[1] = dO[u].x[0] = dO[u].x[1] = dq[u].x[0] = dq[u].x[1] = bc::splat(0.f);
-            lse2[u] = ndl[u] = bc::splat(0.f);
+        for (int v = 0; v < 4; ++v) {
+            kk[v].x[0] = kk[v].x[1] = vv[v].x[0] = vv[v].x[1] = bc::splat(0.f);
+            dk[v].x[0] = dk[v].x[1] = dv[v].x[0] = dv[v].x[1] = bc::splat(0.f);
         }
+        int tb = tb0;
+        asm volatile("" : "+v"(tb));   // recompute the lane's token coordinates per window (hoisted, they spill)
         if (lane_ok) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const TokenInfo ti = token_info(g, w, tb0 + (u & 1) * 18 + (u >> 1) * 108);
-                rowk[u] = ti.row;
-                rq[u] = bc::region_code(reg, bz + 3 * (u >> 1), by + 3 * (u & 1), bx);
-                const float4 kr = *reinterpret_cast<const float4*>(a.k + ti.row * a.ks + coff);
-                const float4 vr = *reinterpret_cast<const float4*>(a.v + ti.row * a.vs + coff);
-                q[u] = bc::load_row_pk(a.q + ti.row * a.qs + coff);
-                dO[u] = bc::load_row_pk(a.dout + ti.row * a.os + coff);
-                const Row o = bc::load_row_pk(a.o + ti.row * a.os + coff);
-                q[u].x[0] *= qscale;
-                q[u].x[1] *= qscale;
-                ndl[u] = -bc::pfma(o.x[0], dO[u].x[0], o.x[1] * dO[u].x[1]);
-                lse2[u] = (f2){a.lse[ti.row * NHT + 2 * wk.hp], a.lse[ti.row * NHT + 2 * wk.hp + 1]} * kLog2e;
-                char* rec = sm + kvw + beta * REC + u * 32;   // key u of quad beta
-                *reinterpret_cast<bc::f4*>(rec) = (bc::f4){kr.x, kr.z, kr.y, kr.w};
-                *reinterpret_cast<bc::f4*>(rec + 16) = (bc::f4){vr.x, vr.z, vr.y, vr.w};
+            for (int v = 0; v < 4; ++v) {
+                const TokenInfo ti = token_info(g, w, tb + (v & 1) * 18 + (v >> 1) * 108);
+                row[v] = ti.row;
+                rk[v] = bc::region_code(reg, bz + 3 * (v >> 1), by + 3 * (v & 1), bx);
+                kk[v] = bc::load_row_pk(a.k + ti.row * a.ks + coff);
+                vv[v] = bc::load_row_pk(a.v + ti.row * a.vs + coff);
             }
         }
-        asm volatile("" ::: "memory");   // the records are written before the walk reads them
-        bool ok = true;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ok = ok && bc::fold_ok(lse2[u]);
-        const bool fold = __all(ok);
-        if (fold) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const f2 e = bc::exp2_2(-lse2[u]);
-                dO[u].x[0] *= e;
-                dO[u].x[1] *= e;
-                ndl[u] *= e;
-            }
+        // half A: quad rows 0-4 (ring slots 0-29), half B: rows 5-8 (slots 0-23)
+#define MMNI_Q4K(M, F, R0, R1, RB) q4k_walk<M, F>(R0, R1, kk, vv, dk, dv, rk, reg, sm, RB, dtw, lane_e, live)
+#define MMNI_WALK(R0, R1, RB)                                                       \
+    do {                                                                        \
+        if (fold) {                                                             \
+            if (reg.masked) MMNI_Q4K(true, true, R0, R1, RB);                   \
+            else MMNI_Q4K(false, true, R0, R1, RB);                             \
+        } else {                                                                \
+            if (reg.masked) MMNI_Q4K(true, false, R0, R1, RB);                  \
+            else MMNI_Q4K(false, false, R0, R1, RB);                            \
+        }                                                                       \
+    } while (0)
+        for (int half = 0; half < 2; ++half) {
+            const int r0 = half ? k4::HALF_ROWS : 0, r1 = half ? 9 : k4::HALF_ROWS;
+            const bool mine = lane_ok && brow >= r0 && brow < r1;
+            const int slot_off = recw + (beta - 6 * r0) * k4::REC;
+            const bool fold = q4k_stage(a, mine, slot_off, row, coff, wk.hp, NHT, qscale);
+            MMNI_WALK(r0, r1, recw);
+            q4k_flush(a, mine, sm + slot_off, row, coff);
         }
-#define MMNI_Q4M(M, F) q4M_loop<M, F>(q, dO, lse2, ndl, dq, lcode, rq, reg, sm, kvw, dtw, lane_ok)
-        if (fold) {
-            if (reg.masked) MMNI_Q4M(true, true);
-            else MMNI_Q4M(false, true);
-        } else {
-            if (reg.masked) MMNI_Q4M(true, false);
-            else MMNI_Q4M(false, false);
-        }
-#undef MMNI_Q4M
+#undef MMNI_WALK
+#undef MMNI_Q4K
         if (lane_ok) {
-            // dq from registers; dk / dv of this lane's key quad from its record slot (the walk
-            // left the final sums there), one 16-byte piece per row and kind
-            const char* rec = sm + kvw + beta * REC;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                bc::store_row_nat(a.dq + rowk[u] * a.qs + coff, dq[u], a.scale);
-                const bc::f4 dkr = *reinterpret_cast<const bc::f4*>(rec + u * 32);
-                const bc::f4 dvr = *reinterpret_cast<const bc::f4*>(rec + u * 32 + 16);
-                *reinterpret_cast<bc::f4*>(a.dk + rowk[u] * a.ks + coff) = dkr * kLn2;   // q carried scale * log2 e
-                *reinterpret_cast<bc::f4*>(a.dv + rowk[u] * a.vs + coff) = dvr;
+            for (int v = 0; v < 4; ++v) {
+                bc::store_row_nat(a.dk + row[v] * a.ks + coff, dk[v], kLn2);   // q carried scale * log2 e
+                bc::store_row_nat(a.dv + row[v] * a.vs + coff, dv[v], 1.0f);
             }
         }
-        asm volatile("" ::: "memory");   // the next window's records stay behind this walk's reads
     }
     __syncthreads();
     float* prow = part + (int64_t)blockIdx.x * TSZ * NHT;
@@ -776,12 +835,12 @@ int wattn_bc_backward(WAArgs& a, int heads, float* dtable, void* workspace, hipS
     const int NHG = heads / 2;
     a.hsplit = NHG;
     const int grid = q4_blocks(2, NHG);
-    int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_bwd_q4m_kernel), q4::LDS_A);
+    int rc = set_lds_limit(reinterpret_cast<const void*>(&wattn_bwd_q4k_kernel), k4::LDS);
     if (rc) return rc;
     const int ncol = g.Tsz * heads;
     float* part = static_cast<float*>(workspace);          // [grid][Tsz * heads]
-    wattn_bwd_q4m_kernel<<<grid, q4::WAVES * 64, q4::LDS_A, s>>>(a, part);
-    rc = launch_status("wattn_bwd_q4m");
+    wattn_bwd_q4k_kernel<<<grid, k4::WAVES * 64, k4::LDS, s>>>(a, part);
+    rc = launch_status("wattn_bwd_q4k");
     if (rc) return rc;
     ColSegs segs{};   // dtable += the fixed-order column sums of the workgroups' partial rows
     segs.n = 1;

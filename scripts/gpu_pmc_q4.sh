@@ -1,16 +1,16 @@
 #!/bin/bash
-# SQ counters and HBM traffic of the merged window-attention backward (wattn_bwd_q4m) for the
+# SQ counters and HBM traffic of the merged window-attention backward (wattn_bwd_q4m / q4k) for the
 # current library and build/base.so (the round-2 kernel: per-step readlane + global dk/dv stores,
 # DPP reduction stages as separate moves), on the C3 micro-benchmark shape.  One counter pass per
 # rocprofv3 run (FETCH_SIZE and WRITE_SIZE cannot share a pass).  usage: gpu_pmc_q4m.sh TAG
 R="$GRAFT_REPO_ROOT"
 TAG=${1:-q4m}
-out="$R/gpurun_out/pmc_q4m_$TAG"
+out="$R/gpurun_out/pmc_q4_$TAG"
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 run() {  # variant lib pass counters...
   local v=$1 lib=$2 n=$3; shift 3
-  MMNI_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "wattn_bwd_q4m" -f csv \
+  MMNI_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "wattn_bwd_q4" -f csv \
       -d "$out/$v/$n" -o w -- python3 "$R/scripts/bench_wattn.py" 3 > "$out/$v/$n.log" 2>&1
   local rc=$?; echo "$v $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$out/$v/$n.log"; exit $rc; }
 }

@@ -60,7 +60,7 @@ import json; d=json.loads(open('gpurun_out/bench_c5_$TAG.json').read().strip().s
 print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_ms'])" ; tail -2 gpurun_out/bench_c5_$TAG.err
   fatal $rc && exit $rc
 fi
-for c in c2 c5; do
+for c in c2 c3 c5; do
   if has bench$c; then
     timeout -k 10 600 python bench.py --config $c --steps 20 --warmup 5 > gpurun_out/bench_${c}_$TAG.json 2> gpurun_out/bench_${c}_$TAG.err
     rc=$?; echo "bench $c rc=$rc"; tail -1 gpurun_out/bench_${c}_$TAG.json | cut -c1-600; tail -2 gpurun_out/bench_${c}_$TAG.err

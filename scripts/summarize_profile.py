@@ -26,7 +26,7 @@ def bench_key(name):
     m = re.search(r"mmni::(wattn_(?:fwd|bwd))_pk2?_kernel<(\d+), (\d), \d+>", name)
     if m:
         return f"{m.group(1)}_k{m.group(3)}_C{m.group(2)}"
-    m = re.search(r"mmni::wattn_bwd[AB]_bc_kernel<6, 6, 6>|mmni::wattn_bwd[AB]_q4_kernel|mmni::wattn_bwd_q4m_kernel", name)
+    m = re.search(r"mmni::wattn_bwd[AB]_bc_kernel<6, 6, 6>|mmni::wattn_bwd[AB]_q4_kernel|mmni::wattn_bwd_q4m_kernel|mmni::wattn_bwd_q4k_kernel", name)
     if m:   # kind 0, C = 12, 6^3 windows: the merged backward (older rounds: passes A + B) = one call
         return "wattn_bwd_k0_C12"
     m = re.search(r"mmni::(mha_\w+?)_kernel<(\d+)>", name)
