@@ -115,12 +115,18 @@ constexpr int MT = 64;      // rows per LDS tile and per workgroup (4 waves x 16
 template <int HDP, int TERMS = 3>
 struct Geo {
     static constexpr int NX = (TERMS * HDP + 31) / 32;   // S-type MFMAs per 16 x 16 sub-tile
-    static constexpr int XS = 32 * NX + 8;           // ext image row stride (bf16): 80 / 144 B, conflict-free
+    // CMP: one bf16 term of d >= 8 -- the ext row holds only the d live values (16 / 32 B) instead of
+    // a zero-padded K = 32 row.  Lanes past K = d read live data of their own row (8 (lg mod d/8)):
+    // the register side is zero there, so those products vanish.  Each ds_read_b128 lane group then
+    // covers the 16 rows once: no bank conflicts (a padded 80-B row measured 41% conflict cycles).
+    static constexpr bool CMP = TERMS == 1 && HDP >= 8;
+    static constexpr int XS = CMP ? HDP : 32 * NX + 8;   // ext image row stride in LDS (bf16)
     static constexpr bool RS = TERMS == 3 && HDP <= 8;   // Z image: row-split (one MFMA per 16 rows)
     static constexpr int ZS = RS ? 136 : 72;         // Z image row stride (bf16): 272 / 144 B
     // Z image rows (RS: hi 0-7, lo 8-15; 3 terms, d = 16: hi 0-15, lo 16-31; 1 term: 0-15)
     static constexpr int ZR = TERMS == 1 ? 16 : (RS ? 16 : 32);
-    static constexpr int EW = 32 * NX;               // ext image row in global (unpadded)
+    static constexpr int EW = CMP ? HDP : 32 * NX;   // ext image row in global (unpadded)
+    static constexpr int XPAD = XS - EW;             // LDS row padding of the ext image (bf16)
     static constexpr int ZW = RS ? 128 : 64;         // Z image row in global (unpadded)
     static constexpr int XT = MT * EW;               // ext tile (bf16 elements)
     static constexpr int ZT = ZR * ZW;               // Z tile (bf16 elements)
@@ -339,9 +345,9 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
     }
 }
 
-// copy one tile image (global rows of W bf16) into LDS (rows of W + 8 bf16), in two halves so
+// copy one tile image (global rows of W bf16) into LDS (rows of W + PAD bf16), in two halves so
 // the next tile's loads are in flight during the current tile's MFMAs
-template <int ROWS, int W>
+template <int ROWS, int W, int PAD = 8>
 struct TileCopy {
     static constexpr int CPR = W / 8;           // 16-byte chunks per row
     static constexpr int N = ROWS * CPR;
@@ -360,7 +366,7 @@ struct TileCopy {
             const int e = tid + 256 * it;
             if (N % 256 == 0 || e < N) {
                 const int row = e / CPR, c = e - row * CPR;
-                *reinterpret_cast<u4*>(l + row * (W + 8) + c * 8) = r[it];
+                *reinterpret_cast<u4*>(l + row * (W + PAD) + c * 8) = r[it];
             }
         }
     }
@@ -389,12 +395,17 @@ __device__ __forceinline__ void build_y(const float (&v)[HDP], int lg, u4 (&y)[G
 
 // S-type: acc += X[16 st + (lane & 15)][:] . Y[:]  over the 3-term ext dimension
 template <int HDP, int TERMS>
+__device__ __forceinline__ int xcol(int c, int lg) {
+    using G = Geo<HDP, TERMS>;
+    return G::CMP ? 8 * (lg % (HDP / 8)) : 32 * c + 8 * lg;
+}
+template <int HDP, int TERMS>
 __device__ __forceinline__ mf4 sprod(const uint16_t* xe, int st, const u4 (&y)[Geo<HDP, TERMS>::NX], mf4 acc,
                                      int ln, int lg) {
     using G = Geo<HDP, TERMS>;
 #pragma unroll
     for (int c = 0; c < G::NX; ++c)
-        acc = mfma_bf(*reinterpret_cast<const u4*>(xe + (16 * st + ln) * G::XS + 32 * c + 8 * lg), y[c], acc);
+        acc = mfma_bf(*reinterpret_cast<const u4*>(xe + (16 * st + ln) * G::XS + xcol<HDP, TERMS>(c, lg)), y[c], acc);
     return acc;
 }
 
@@ -530,7 +541,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vzg = a.vz + (int64_t)bh * a.nkt * G::ZT;
-    TileCopy<MT, G::EW> ck;
+    TileCopy<MT, G::EW, G::XPAD> ck;
     TileCopy<G::ZR, G::ZW> cv;
     mf4 o = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
@@ -659,7 +670,7 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vxg = a.vx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* kzg = a.kz + (int64_t)bh * a.nkt * G::ZT;
-    TileCopy<MT, G::EW> ck, cv;
+    TileCopy<MT, G::EW, G::XPAD> ck, cv;
     TileCopy<G::ZR, G::ZW> cz;
     const mf4 sinit = {-lse2, -lse2, -lse2, -lse2};
     const float di = DROP ? 0.f : -dl;
@@ -756,7 +767,7 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
     const uint16_t* gxg = a.gx + (int64_t)bh * a.nqt * G::XT;
     const uint16_t* qzg = a.qz + (int64_t)bh * a.nqt * G::ZT;
     const uint16_t* gzg = a.gz + (int64_t)bh * a.nqt * G::ZT;
-    TileCopy<MT, G::EW> cq, cg;
+    TileCopy<MT, G::EW, G::XPAD> cq, cg;
     TileCopy<G::ZR, G::ZW> czq, czg;
     float pl = 0.f, pd_ = 0.f;   // the tile's -lse2 / -delta (threads < MT)
     mf4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
@@ -946,7 +957,7 @@ struct MhaWs {
 static MhaWs mha_ws_layout(const MhaArgs& a, bool bwd) {
     const int HDP = hd_pad(a.hd), TERMS = a.bf16 ? 1 : 3;
     const bool RS = TERMS == 3 && HDP <= 8;
-    const int NX = (TERMS * HDP + 31) / 32, EW = 32 * NX, ZR = TERMS == 1 ? 16 : (RS ? 16 : 32), ZW = RS ? 128 : 64;
+    const int NX = (TERMS * HDP + 31) / 32, EW = (TERMS == 1 && HDP >= 8) ? HDP : 32 * NX, ZR = TERMS == 1 ? 16 : (RS ? 16 : 32), ZW = RS ? 128 : 64;
     const size_t bhn = (size_t)a.B * a.H, xt = (size_t)MT * EW * 2, zt = (size_t)ZR * ZW * 2;
     const size_t nk = bhn * ((a.Tk + MT - 1) / MT), nq = bhn * ((a.Tq + MT - 1) / MT);
     MhaWs w{};
