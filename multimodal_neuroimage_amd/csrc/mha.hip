@@ -122,9 +122,13 @@ struct Geo {
     static constexpr bool CMP = TERMS == 1 && HDP >= 8;
     static constexpr int XS = CMP ? HDP : 32 * NX + 8;   // ext image row stride in LDS (bf16)
     static constexpr bool RS = TERMS == 3 && HDP <= 8;   // Z image: row-split (one MFMA per 16 rows)
-    static constexpr int ZS = RS ? 136 : 72;         // Z image row stride (bf16): 272 / 144 B
+    // Z image row stride (bf16): 272 / 144 B; CMP: 160 B, where the 16 (row, 16-B column) pairs of
+    // every ds_read_b128 lane group fall on distinct bank quads (144 B: 2-way conflicts)
+    static constexpr int ZS = CMP ? 80 : (RS ? 136 : 72);
     // Z image rows (RS: hi 0-7, lo 8-15; 3 terms, d = 16: hi 0-15, lo 16-31; 1 term: 0-15)
-    static constexpr int ZR = TERMS == 1 ? 16 : (RS ? 16 : 32);
+    // CMP: d rows (HDP 8: the MFMA's rows 8-15 re-read rows 0-7; their outputs, dims >= 8, are
+    // never stored)
+    static constexpr int ZR = CMP ? HDP : (TERMS == 1 ? 16 : (RS ? 16 : 32));
     static constexpr int EW = CMP ? HDP : 32 * NX;   // ext image row in global (unpadded)
     static constexpr int XPAD = XS - EW;             // LDS row padding of the ext image (bf16)
     static constexpr int ZW = RS ? 128 : 64;         // Z image row in global (unpadded)
@@ -418,7 +422,7 @@ __device__ __forceinline__ mf4 zprod(const uint16_t* z, const mf4 (&w)[4], mf4 a
         for (int c = 0; c < 2; ++c) {
             const mf4 &wa = w[2 * c], &wb = w[2 * c + 1];
             const u4 B = {pk_rn(wa[0], wa[1]), pk_rn(wa[2], wa[3]), pk_rn(wb[0], wb[1]), pk_rn(wb[2], wb[3])};
-            acc = mfma_bf(*reinterpret_cast<const u4*>(z + ln * G::ZS + c * 32 + lg * 8), B, acc);
+            acc = mfma_bf(*reinterpret_cast<const u4*>(z + (ln & (G::ZR - 1)) * G::ZS + c * 32 + lg * 8), B, acc);
         }
     } else if constexpr (G::RS) {
 #pragma unroll
@@ -542,7 +546,7 @@ __global__ __launch_bounds__(256) void mha_fwd_mfma_kernel(MhaArgs a) {
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vzg = a.vz + (int64_t)bh * a.nkt * G::ZT;
     TileCopy<MT, G::EW, G::XPAD> ck;
-    TileCopy<G::ZR, G::ZW> cv;
+    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW> cv;
     mf4 o = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
     const int kend_blk = key_end(a, min(a.Tq - 1, bx * MT + MT - 1));
@@ -671,7 +675,7 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
     const uint16_t* vxg = a.vx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* kzg = a.kz + (int64_t)bh * a.nkt * G::ZT;
     TileCopy<MT, G::EW, G::XPAD> ck, cv;
-    TileCopy<G::ZR, G::ZW> cz;
+    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW> cz;
     const mf4 sinit = {-lse2, -lse2, -lse2, -lse2};
     const float di = DROP ? 0.f : -dl;
     const mf4 dinit = {di, di, di, di};
@@ -768,7 +772,7 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
     const uint16_t* qzg = a.qz + (int64_t)bh * a.nqt * G::ZT;
     const uint16_t* gzg = a.gz + (int64_t)bh * a.nqt * G::ZT;
     TileCopy<MT, G::EW, G::XPAD> cq, cg;
-    TileCopy<G::ZR, G::ZW> czq, czg;
+    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW> czq, czg;
     float pl = 0.f, pd_ = 0.f;   // the tile's -lse2 / -delta (threads < MT)
     mf4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
     // first query that can see the block's first key: j - i < diag  <=>  i > j - diag
@@ -957,7 +961,8 @@ struct MhaWs {
 static MhaWs mha_ws_layout(const MhaArgs& a, bool bwd) {
     const int HDP = hd_pad(a.hd), TERMS = a.bf16 ? 1 : 3;
     const bool RS = TERMS == 3 && HDP <= 8;
-    const int NX = (TERMS * HDP + 31) / 32, EW = (TERMS == 1 && HDP >= 8) ? HDP : 32 * NX, ZR = TERMS == 1 ? 16 : (RS ? 16 : 32), ZW = RS ? 128 : 64;
+    const int NX = (TERMS * HDP + 31) / 32, EW = (TERMS == 1 && HDP >= 8) ? HDP : 32 * NX,
+              ZR = (TERMS == 1 && HDP >= 8) ? HDP : (TERMS == 1 ? 16 : (RS ? 16 : 32)), ZW = RS ? 128 : 64;
     const size_t bhn = (size_t)a.B * a.H, xt = (size_t)MT * EW * 2, zt = (size_t)ZR * ZW * 2;
     const size_t nk = bhn * ((a.Tk + MT - 1) / MT), nq = bhn * ((a.Tq + MT - 1) / MT);
     MhaWs w{};
