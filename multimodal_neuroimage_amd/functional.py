@@ -988,13 +988,26 @@ class _SplitKLinear(torch.autograd.Function):
     tiny N x K output and K = T*B = 6,912 (C4) to 32,768 (C5) rows, where the library's single
     GEMM tiles only the output and runs a few dozen workgroups (57-114 us a call, profiles/).
     Under bf16 autocast the products run in bf16 like F.linear's; the gradients come back in the
-    parameters' own dtype."""
+    parameters' own dtype.  The autocast casts of x and W are made once, in the forward, and the bf16
+    copies are what the backward keeps (no re-cast per backward), and the fp32 sums of dW's chunks
+    and of db read the bf16 values directly (sum with dtype=float32: no cast pass)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+        ctx.x_dtype = x.dtype
+        if torch.is_autocast_enabled() and x.is_cuda:
+            cdt = torch.get_autocast_gpu_dtype()
+            xc, wc = x.to(cdt), weight.to(cdt)
+            bc = bias.to(cdt) if bias is not None else None
+            with torch.autocast(device_type="cuda", enabled=False):
+                y = F.linear(xc, wc, bc)
+        else:
+            xc, wc = x, weight
+            y = F.linear(x, weight, bias)
+        ctx.save_for_backward(xc, wc)
+        ctx.w_dtype = weight.dtype
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
@@ -1003,7 +1016,7 @@ class _SplitKLinear(torch.autograd.Function):
         N, K = w.shape
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (dy @ w.to(cdt)).to(x.dtype)
+            dx = (dy @ w.to(cdt)).to(ctx.x_dtype)
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K).to(cdt)
         rows = dy2.shape[0]
@@ -1011,11 +1024,11 @@ class _SplitKLinear(torch.autograd.Function):
         S = _splitk_chunks(rows)
         if S > 1:
             r = rows // S
-            dw = torch.bmm(dy2.view(S, r, N).transpose(1, 2), x2.view(S, r, K)).to(acc).sum(0)
+            dw = torch.bmm(dy2.view(S, r, N).transpose(1, 2), x2.view(S, r, K)).sum(0, dtype=acc)
         else:
             dw = (dy2.t() @ x2).to(acc)
-        db = dy2.to(acc).sum(0).to(w.dtype) if ctx.has_bias else None
-        return dx, dw.to(w.dtype), db
+        db = dy2.sum(0, dtype=acc).to(ctx.w_dtype) if ctx.has_bias else None
+        return dx, dw.to(ctx.w_dtype), db
 
 
 def splitk_linear(x, weight, bias=None):

@@ -1,5 +1,7 @@
 """The crossmodal encoder's Linear with a split-K weight gradient (functional.SplitKLinear): the
-row-chunk rule and the gradients against plain autograd, on the CPU (float64)."""
+row-chunk rule and the gradients against plain autograd on the CPU (float64), and its bf16
+autocast path against F.linear's on the GPU."""
+import pytest
 import torch
 
 from multimodal_neuroimage_amd.functional import SplitKLinear, _splitk_chunks, splitk_linear
@@ -36,3 +38,31 @@ def test_module_keeps_linear_state_dict():
     m = SplitKLinear(12, 84)
     assert isinstance(m, torch.nn.Linear)
     assert set(m.state_dict()) == {"weight", "bias"}
+
+
+@pytest.mark.gpu
+def test_bf16_autocast_matches_f_linear():
+    """Under bf16 autocast (C5's head) the split-K Linear casts x and W once in its forward and keeps
+    the bf16 copies: output and gradients match F.linear's autocast path (bf16 products, fp32
+    parameter gradients), and the gradient dtypes follow the inputs'."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    for x_dtype in (torch.float32, torch.bfloat16):
+        x = torch.randn(4096, 2, 84, device=dev, generator=g).to(x_dtype).requires_grad_(True)
+        w = torch.randn(336, 84, device=dev, generator=g).mul_(0.1).requires_grad_(True)
+        b = torch.randn(336, device=dev, generator=g).requires_grad_(True)
+        gy = torch.randn(4096, 2, 336, device=dev, generator=g).to(torch.bfloat16)
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            y = splitk_linear(x, w, b)
+        y.backward(gy)
+        got = (y.detach().float(), x.grad.float(), w.grad, b.grad)
+        assert y.dtype == torch.bfloat16 and x.grad.dtype == x_dtype
+        assert w.grad.dtype == torch.float32 and b.grad.dtype == torch.float32
+        x.grad = w.grad = b.grad = None
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            yr = torch.nn.functional.linear(x, w, b)
+        yr.backward(gy)
+        ref = (yr.detach().float(), x.grad.float(), w.grad, b.grad)
+        for a, r in zip(got, ref):
+            err = float((a - r).abs().max() / r.abs().max())
+            assert err < 2e-2, err
