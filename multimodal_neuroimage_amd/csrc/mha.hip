@@ -351,24 +351,24 @@ __global__ __launch_bounds__(256) void mha_split_kernel(SplitArgs sa) {
 
 // copy one tile image (global rows of W bf16) into LDS (rows of W + PAD bf16), in two halves so
 // the next tile's loads are in flight during the current tile's MFMAs
-template <int ROWS, int W, int PAD = 8>
+template <int ROWS, int W, int PAD = 8, int NT = 256>
 struct TileCopy {
     static constexpr int CPR = W / 8;           // 16-byte chunks per row
     static constexpr int N = ROWS * CPR;
-    static constexpr int IT = (N + 255) / 256;
+    static constexpr int IT = (N + NT - 1) / NT;
     u4 r[IT];
     __device__ __forceinline__ void load(const uint16_t* g, int tid) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int e = tid + 256 * it;
-            if (N % 256 == 0 || e < N) r[it] = *reinterpret_cast<const u4*>(g + e * 8);
+            const int e = tid + NT * it;
+            if (N % NT == 0 || e < N) r[it] = *reinterpret_cast<const u4*>(g + e * 8);
         }
     }
     __device__ __forceinline__ void store(uint16_t* l, int tid) const {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int e = tid + 256 * it;
-            if (N % 256 == 0 || e < N) {
+            const int e = tid + NT * it;
+            if (N % NT == 0 || e < N) {
                 const int row = e / CPR, c = e - row * CPR;
                 *reinterpret_cast<u4*>(l + row * (W + PAD) + c * 8) = r[it];
             }
@@ -643,6 +643,15 @@ struct DqLds {
     static constexpr int NBUF = Stages<STAGE * 2>::N;
     static constexpr int BYTES = NBUF * STAGE * 2;
 };
+// Row groups per wave in the backward: with one bf16 term (CMP) and head_dim <= 8 a wave takes
+// RG = 2 groups of 16 rows (two-wave workgroups of 64 rows), so each tile's LDS operands, copy and
+// barrier serve twice the MFMA and softmax work (T=4096 E84: 0.322 -> 0.312-0.318 ms; at head_dim
+// 16 the halved wave count measured slower, 0.361 -> 0.377 ms, profiles/r3t_mha_ab.txt).
+template <int HDP, int TERMS>
+struct BwdRG {
+    static constexpr int RG = (Geo<HDP, TERMS>::CMP && HDP == 8) ? 2 : 1;
+    static constexpr int NT = 256 / RG;   // threads per workgroup
+};
 template <int HDP, bool DROP, typename T>
 __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int bx, int bh) {
     constexpr int TERMS = kTerms<T>;
@@ -650,38 +659,47 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
     using L = DqLds<HDP, TERMS>;
     constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
     constexpr int NBUF = L::NBUF;
+    constexpr int RG = BwdRG<HDP, TERMS>::RG, NT = BwdRG<HDP, TERMS>::NT;
     (void)SZ;
     const int b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int q0 = bx * MT + wave * 16;
-    const int qi = q0 + ln;
-    const bool qok = qi < a.Tq;
-    const int64_t rq = ((int64_t)qi * a.B + b) * a.qs + h * a.hd, ro = ((int64_t)qi * a.B + b) * a.os + h * a.hd;
-    u4 qy[G::NX], gy[G::NX];
-    {
+    const int q0 = bx * MT + wave * 16 * RG;   // group g: rows q0 + 16 g + ln
+    int qi[RG];
+    bool qok[RG];
+    int64_t rq[RG];
+    u4 qy[RG][G::NX], gy[RG][G::NX];
+    float dl[RG];
+    uint32_t rowh[RG];
+    mf4 sinit[RG], dinit[RG], dq[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+        qi[g] = q0 + 16 * g + ln;
+        qok[g] = qi[g] < a.Tq;
+        rq[g] = ((int64_t)qi[g] * a.B + b) * a.qs + h * a.hd;
+        const int64_t ro = ((int64_t)qi[g] * a.B + b) * a.os + h * a.hd;
         float qv[HDP], gv[HDP];
 #pragma unroll
         for (int d = 0; d < HDP; ++d) {
-            qv[d] = load_pad<T>(a.q, rq, d, a.hd, qok) * a.scale2;
-            gv[d] = load_pad<T>(a.dout, ro, d, a.hd, qok);
+            qv[d] = load_pad<T>(a.q, rq[g], d, a.hd, qok[g]) * a.scale2;
+            gv[d] = load_pad<T>(a.dout, ro, d, a.hd, qok[g]);
         }
-        build_y<HDP, TERMS>(qv, lg, qy);
-        build_y<HDP, TERMS>(gv, lg, gy);
+        build_y<HDP, TERMS>(qv, lg, qy[g]);
+        build_y<HDP, TERMS>(gv, lg, gy[g]);
+        const float lse2 = qok[g] ? a.lse[(int64_t)bh * a.Tq + qi[g]] * kLog2e : INFINITY;
+        dl[g] = qok[g] ? a.delta[(int64_t)bh * a.Tq + qi[g]] : 0.f;
+        rowh[g] = DROP ? drop_row(a.seed, bh, a.Tq, qi[g]) : 0u;
+        sinit[g] = (mf4){-lse2, -lse2, -lse2, -lse2};
+        const float di = DROP ? 0.f : -dl[g];
+        dinit[g] = (mf4){di, di, di, di};
+        dq[g] = (mf4){0.f, 0.f, 0.f, 0.f};
     }
-    const float lse2 = qok ? a.lse[(int64_t)bh * a.Tq + qi] * kLog2e : INFINITY;
-    const float dl = qok ? a.delta[(int64_t)bh * a.Tq + qi] : 0.f;
-    const uint32_t rowh = DROP ? drop_row(a.seed, bh, a.Tq, qi) : 0u;
     const uint16_t* kxg = a.kx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* vxg = a.vx + (int64_t)bh * a.nkt * G::XT;
     const uint16_t* kzg = a.kz + (int64_t)bh * a.nkt * G::ZT;
-    TileCopy<MT, G::EW, G::XPAD> ck, cv;
-    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW> cz;
-    const mf4 sinit = {-lse2, -lse2, -lse2, -lse2};
-    const float di = DROP ? 0.f : -dl;
-    const mf4 dinit = {di, di, di, di};
-    mf4 dq = {0.f, 0.f, 0.f, 0.f};
+    TileCopy<MT, G::EW, G::XPAD, NT> ck, cv;
+    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW, NT> cz;
     const int kend_blk = key_end(a, min(a.Tq - 1, bx * MT + MT - 1));
-    const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 15)) : 0;
+    const int kend_w = q0 < a.Tq ? key_end(a, min(a.Tq - 1, q0 + 16 * RG - 1)) : 0;
     tile_loop<NBUF>(
         0, (kend_blk + MT - 1) / MT,
         [&](int t) {
@@ -701,33 +719,41 @@ __device__ __forceinline__ void mha_dq_body(const MhaArgs& a, uint16_t* lds, int
             const uint16_t* kx = lds + buf * STAGE;
             const uint16_t* vx = kx + SX;
             const uint16_t* kz = kx + 2 * SX;
-            mf4 s[4], dp[4];
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                s[st] = sprod<HDP, TERMS>(kx, st, qy, sinit, ln, lg);    // S^T - lse2
-                dp[st] = sprod<HDP, TERMS>(vx, st, gy, dinit, ln, lg);   // dP^T (- delta)
-            }
-            const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > q0 + a.causal);
-            if (edge) mask_keys(s, k0, qi, lg, a);
+            for (int g = 0; g < RG; ++g) {
+                const int qg = q0 + 16 * g;
+                if (RG > 1 && k0 >= key_end(a, min(a.Tq - 1, qg + 15))) continue;   // wave-uniform
+                mf4 s[4], dp[4];
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int j = k0 + 16 * st + 4 * lg + i;
-                    const float p = fast_exp2(s[st][i]);
-                    float g = dp[st][i];
-                    if (DROP) g = (drop_keep(rowh, j, a.thresh) ? g * a.inv_keep : 0.f) - dl;
-                    s[st][i] = p * g;   // dS^T
+                for (int st = 0; st < 4; ++st) {
+                    s[st] = sprod<HDP, TERMS>(kx, st, qy[g], sinit[g], ln, lg);    // S^T - lse2
+                    dp[st] = sprod<HDP, TERMS>(vx, st, gy[g], dinit[g], ln, lg);   // dP^T (- delta)
                 }
-            }
-            dq = zprod<HDP, TERMS>(kz, s, dq, ln, lg);   // dQ^T += K^T dS^T
-        });
-    dq = zfinish<HDP, TERMS>(dq);
-    if (qok && zrow_owner<HDP, TERMS>(lg)) {
+                const bool edge = (k0 + MT > a.Tk) || (a.causal > 0 && k0 + MT > qg + a.causal);
+                if (edge) mask_keys(s, k0, qi[g], lg, a);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
-            if (d < a.hd) stf<T>(a.dq, rq + d, dq[i] * a.scale);
+                for (int st = 0; st < 4; ++st) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int j = k0 + 16 * st + 4 * lg + i;
+                        const float p = fast_exp2(s[st][i]);
+                        float gg = dp[st][i];
+                        if (DROP) gg = (drop_keep(rowh[g], j, a.thresh) ? gg * a.inv_keep : 0.f) - dl[g];
+                        s[st][i] = p * gg;   // dS^T
+                    }
+                }
+                dq[g] = zprod<HDP, TERMS>(kz, s, dq[g], ln, lg);   // dQ^T += K^T dS^T
+            }
+        });
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+        const mf4 dqf = zfinish<HDP, TERMS>(dq[g]);
+        if (qok[g] && zrow_owner<HDP, TERMS>(lg)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
+                if (d < a.hd) stf<T>(a.dq, rq[g] + d, dqf[i] * a.scale);
+            }
         }
     }
 }
@@ -750,31 +776,38 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
     using L = DkvLds<HDP, TERMS>;
     constexpr int SX = L::SX, SZ = L::SZ, STAGE = L::STAGE;
     constexpr int NBUF = L::NBUF;
+    constexpr int RG = BwdRG<HDP, TERMS>::RG, NT = BwdRG<HDP, TERMS>::NT;
     const int b = bh / a.H, h = bh % a.H;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, ln = l & 15, lg = l >> 4;
-    const int j0 = bx * MT + wave * 16;
-    const int kj = j0 + ln;
-    const bool kok = kj < a.Tk;
-    const int64_t rk = ((int64_t)kj * a.B + b) * a.ks + h * a.hd, rv = ((int64_t)kj * a.B + b) * a.vs + h * a.hd;
-    u4 ky[G::NX], vy[G::NX];
-    {
+    const int j0 = bx * MT + wave * 16 * RG;   // group g: keys j0 + 16 g + ln
+    int kj[RG];
+    bool kok[RG];
+    int64_t rk[RG], rv[RG];
+    u4 ky[RG][G::NX], vy[RG][G::NX];
+    mf4 dk[RG], dv[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+        kj[g] = j0 + 16 * g + ln;
+        kok[g] = kj[g] < a.Tk;
+        rk[g] = ((int64_t)kj[g] * a.B + b) * a.ks + h * a.hd;
+        rv[g] = ((int64_t)kj[g] * a.B + b) * a.vs + h * a.hd;
         float kv[HDP], vv[HDP];
 #pragma unroll
         for (int d = 0; d < HDP; ++d) {
-            kv[d] = load_pad<T>(a.k, rk, d, a.hd, kok);
-            vv[d] = load_pad<T>(a.v, rv, d, a.hd, kok);
+            kv[d] = load_pad<T>(a.k, rk[g], d, a.hd, kok[g]);
+            vv[d] = load_pad<T>(a.v, rv[g], d, a.hd, kok[g]);
         }
-        build_y<HDP, TERMS>(kv, lg, ky);
-        build_y<HDP, TERMS>(vv, lg, vy);
+        build_y<HDP, TERMS>(kv, lg, ky[g]);
+        build_y<HDP, TERMS>(vv, lg, vy[g]);
+        dk[g] = dv[g] = (mf4){0.f, 0.f, 0.f, 0.f};
     }
     const uint16_t* qxg = a.qx + (int64_t)bh * a.nqt * G::XT;
     const uint16_t* gxg = a.gx + (int64_t)bh * a.nqt * G::XT;
     const uint16_t* qzg = a.qz + (int64_t)bh * a.nqt * G::ZT;
     const uint16_t* gzg = a.gz + (int64_t)bh * a.nqt * G::ZT;
-    TileCopy<MT, G::EW, G::XPAD> cq, cg;
-    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW> czq, czg;
+    TileCopy<MT, G::EW, G::XPAD, NT> cq, cg;
+    TileCopy<G::ZR, G::ZW, G::ZS - G::ZW, NT> czq, czg;
     float pl = 0.f, pd_ = 0.f;   // the tile's -lse2 / -delta (threads < MT)
-    mf4 dk = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
     // first query that can see the block's first key: j - i < diag  <=>  i > j - diag
     int i_begin = 0;
     if (a.causal > 0) i_begin = max(0, bx * MT - a.causal + 1);
@@ -813,61 +846,74 @@ __device__ __forceinline__ void mha_dkv_body(const MhaArgs& a, uint16_t* lds, in
             const uint16_t* gz = qz + SZ;
             const float* ls_ = reinterpret_cast<const float*>(qx + 2 * SX + 2 * SZ);
             const float* ds_ = ls_ + MT;
-            mf4 s[4], dp[4];
+            mf4 li[4], di[4];   // the rows' -lse2 / -delta, shared by the groups
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
                 const float2 l01 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg);
                 const float2 l23 = *reinterpret_cast<const float2*>(ls_ + 16 * st + 4 * lg + 2);
-                s[st] = sprod<HDP, TERMS>(qx, st, ky, (mf4){l01.x, l01.y, l23.x, l23.y}, ln, lg);   // S - lse2
-                mf4 di = {0.f, 0.f, 0.f, 0.f};
+                li[st] = (mf4){l01.x, l01.y, l23.x, l23.y};
+                di[st] = (mf4){0.f, 0.f, 0.f, 0.f};
                 if (!DROP) {
                     const float2 d01 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg);
                     const float2 d23 = *reinterpret_cast<const float2*>(ds_ + 16 * st + 4 * lg + 2);
-                    di = (mf4){d01.x, d01.y, d23.x, d23.y};
+                    di[st] = (mf4){d01.x, d01.y, d23.x, d23.y};
                 }
-                dp[st] = sprod<HDP, TERMS>(gx, st, vy, di, ln, lg);   // dP (- delta)
             }
-            // lane: s[st][i] = S[query i0 + 16 st + 4 lg + i][key kj]
-            const bool edge = (i0 + MT > a.Tq) || !kok || (a.causal > 0 && i0 < j0 + 16 - a.causal + 1);
-            if (edge) {
 #pragma unroll
-                for (int st = 0; st < 4; ++st)
+            for (int g = 0; g < RG; ++g) {
+                const int jg = j0 + 16 * g;
+                if (RG > 1 && (jg >= a.Tk || (a.causal > 0 && i0 + MT <= jg - a.causal + 1))) continue;   // wave-uniform
+                mf4 s[4], dp[4];
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    s[st] = sprod<HDP, TERMS>(qx, st, ky[g], li[st], ln, lg);    // S - lse2
+                    dp[st] = sprod<HDP, TERMS>(gx, st, vy[g], di[st], ln, lg);   // dP (- delta)
+                }
+                // lane: s[st][i] = S[query i0 + 16 st + 4 lg + i][key kj]
+                const bool edge = (i0 + MT > a.Tq) || !kok[g] || (a.causal > 0 && i0 < jg + 16 - a.causal + 1);
+                if (edge) {
+#pragma unroll
+                    for (int st = 0; st < 4; ++st)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int qi = i0 + 16 * st + 4 * lg + i;
+                            const bool mk = (qi >= a.Tq) | !kok[g] | ((a.causal > 0) & (kj[g] - qi >= a.causal));
+                            s[st][i] = mk ? -INFINITY : s[st][i];
+                        }
+                }
+                mf4 pd[4];
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int qi = i0 + 16 * st + 4 * lg + i;
-                        const bool mk = (qi >= a.Tq) | !kok | ((a.causal > 0) & (kj - qi >= a.causal));
-                        s[st][i] = mk ? -INFINITY : s[st][i];
+                        const int r = 16 * st + 4 * lg + i, qi = i0 + r;
+                        const float p = fast_exp2(s[st][i]);
+                        float gg = dp[st][i], pv = p;
+                        if (DROP) {
+                            const bool kp = drop_keep(drop_row(a.seed, bh, a.Tq, qi), kj[g], a.thresh);
+                            gg = (kp ? gg * a.inv_keep : 0.f) + ds_[r];
+                            pv = kp ? p * a.inv_keep : 0.f;
+                        }
+                        pd[st][i] = pv;
+                        s[st][i] = p * gg;   // dS
                     }
-            }
-            mf4 pd[4];
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = 16 * st + 4 * lg + i, qi = i0 + r;
-                    const float p = fast_exp2(s[st][i]);
-                    float g = dp[st][i], pv = p;
-                    if (DROP) {
-                        const bool kp = drop_keep(drop_row(a.seed, bh, a.Tq, qi), kj, a.thresh);
-                        g = (kp ? g * a.inv_keep : 0.f) + ds_[r];
-                        pv = kp ? p * a.inv_keep : 0.f;
-                    }
-                    pd[st][i] = pv;
-                    s[st][i] = p * g;   // dS
                 }
+                dv[g] = zprod<HDP, TERMS>(gz, pd, dv[g], ln, lg);   // dV^T += dO^T Pd
+                dk[g] = zprod<HDP, TERMS>(qz, s, dk[g], ln, lg);    // dK^T += Q2^T dS
             }
-            dv = zprod<HDP, TERMS>(gz, pd, dv, ln, lg);   // dV^T += dO^T Pd
-            dk = zprod<HDP, TERMS>(qz, s, dk, ln, lg);    // dK^T += Q2^T dS
         });
-    dk = zfinish<HDP, TERMS>(dk);
-    dv = zfinish<HDP, TERMS>(dv);
-    if (kok && zrow_owner<HDP, TERMS>(lg)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
-            if (d < a.hd) {
-                stf<T>(a.dk, rk + d, dk[i] * kLn2);   // staged q2 = q * scale * log2e
-                stf<T>(a.dv, rv + d, dv[i]);
+    for (int g = 0; g < RG; ++g) {
+        const mf4 dkf = zfinish<HDP, TERMS>(dk[g]);
+        const mf4 dvf = zfinish<HDP, TERMS>(dv[g]);
+        if (kok[g] && zrow_owner<HDP, TERMS>(lg)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = 4 * (G::RS ? (lg & 1) : lg) + i;
+                if (d < a.hd) {
+                    stf<T>(a.dk, rk[g] + d, dkf[i] * kLn2);   // staged q2 = q * scale * log2e
+                    stf<T>(a.dv, rv[g] + d, dvf[i]);
+                }
             }
         }
     }
@@ -1031,7 +1077,8 @@ static int mha_bwd_launch(MhaArgs& a, char* ws, hipStream_t s) {
     constexpr int TERMS = kTerms<T>;
     const int lds = DqLds<HDP, TERMS>::BYTES > DkvLds<HDP, TERMS>::BYTES ? DqLds<HDP, TERMS>::BYTES
                                                                          : DkvLds<HDP, TERMS>::BYTES;
-    mha_bwd_mfma_kernel<HDP, DROP, T><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H, 2), 256, lds, s>>>(a);
+    mha_bwd_mfma_kernel<HDP, DROP, T><<<dim3(a.nkt > a.nqt ? a.nkt : a.nqt, a.B * a.H, 2),
+                                         BwdRG<HDP, kTerms<T>>::NT, lds, s>>>(a);
     return launch_status("mha_bwd");
 }
 

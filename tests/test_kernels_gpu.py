@@ -250,6 +250,8 @@ MHA_BF16 = [
     (64, 96, 1, 4, 8, False),
     (130, 130, 1, 6, 4, True),
     (1024, 1024, 1, 12, 7, True),
+    (96, 80, 1, 3, 16, True),     # compact images at d = 16 (no padding dims)
+    (77, 77, 2, 5, 11, True),     # d = 11: padded to 16, partial last tile
 ]
 TOL_BF16 = 2e-2   # bf16 runs are held to 2e-2 rel against the fp32/fp64 golden
 
