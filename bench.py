@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--checkpoint", action="store_true", help="recompute blocks in backward (memory)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd + bwd + AdamW) in one hipGraph and replay it (N = 1 only); "
-                         "the default for the launch-bound configs c2 and c4 when --gpus is not given")
+                         "the default for the launch-bound configs c2, c4 and c5 when --gpus is not given")
     ap.add_argument("--eager", action="store_true",
                     help="no hipGraph capture.  Implied whenever --gpus is given (so a 1/2/4/8-GPU curve compares "
                          "eager steps at every N: the DDP step is not captured)")
@@ -330,11 +330,11 @@ def main():
     else:
         kw = model_kwargs(args.size)
         model = D.wrap_ddp(M.SwinFusion(use_checkpoint=args.checkpoint, **kw).to(device), env)
-    # hipGraph policy: explicit --graph (N = 1), or the c2 / c4 default when no --gpus was given; a
+    # hipGraph policy: explicit --graph (N = 1), or the c2 / c4 / c5 default when no --gpus was given; a
     # --gpus run is eager at every N so the driver's 1 -> N curve compares like with like
     if args.graph and world > 1:
         raise SystemExit("bench.py: --graph captures a single-process step (N = 1); the DDP step runs eager")
-    graph = args.graph or (args.config in ("c2", "c4") and not args.eager and args.gpus is None and world == 1)
+    graph = args.graph or (args.config in ("c2", "c4", "c5") and not args.eager and args.gpus is None and world == 1)
     if graph:
         # a captured step replays the host-drawn attention-dropout seed of the capture: refuse rather
         # than train with one frozen mask (multihead_attention.py draws one per forward)
