@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MMNI_ABI_VERSION 7
+#define MMNI_ABI_VERSION 8
 
 /* ------------------------------------------------------------------------------------
  * Shifted-window attention.
@@ -375,6 +375,20 @@ int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn,
                            const float* gamma, const float* mean, const float* rstd, const float* dres,
                            int64_t ldres, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace,
                            void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Split-K weight-gradient reductions (ABI v8) of the crossmodal encoder's Linears
+ * (crossmodal_transformer.py:189-194 Linear, multihead_attention.py in_proj / out_proj: the
+ * backward of F.linear, whose weight gradient the host runs as one batched GEMM over S row chunks):
+ *   dw[e] = sum_{c < S} part[c][e]   (e < NK = N * K; chunk order)
+ *   db[n] = sum_{r < rows} dy[r][n]  (row stride ldy; fixed row slabs + fixed-order slab sum; db,
+ *                                     dy nullable together)
+ * part and dy are fp32 (dtype 0) or bf16 (dtype 1, the autocast head); sums and outputs fp32.
+ * Bitwise deterministic.  Workspace: mmni_splitk_reduce_workspace_bytes(rows, N).
+ * ------------------------------------------------------------------------------------ */
+size_t mmni_splitk_reduce_workspace_bytes(int64_t rows, int N);
+int mmni_splitk_reduce(int S, int64_t NK, const void* part, int64_t rows, int N, const void* dy, int64_t ldy,
+                       int dtype, float* dw, float* db, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Swin-V2 continuous position bias table (ABI v7; replaces WindowAttention.cpb_mlp applied to

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MMNI_LIB selects another in-tree build of the same library (kernel experiments,
 # scripts/build_variant.sh); the default is the package's libmmni.so.
 LIB_PATH = os.environ.get("MMNI_LIB") or os.path.join(_HERE, "libmmni.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _c_int = ctypes.c_int
 _c_i32 = ctypes.c_int32
@@ -83,6 +83,8 @@ SIGNATURES = {
     "mmni_cpb_bwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 11),
     "mmni_row_layernorm_bwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp,
                                         _c_i64, _vp, _vp, _vp, _vp]),
+    "mmni_splitk_reduce_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
+    "mmni_splitk_reduce": (_c_int, [_c_int, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
     "mmni_last_error": (ctypes.c_char_p, []),
     "mmni_wattn_fwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 9),
     "mmni_wattn_bwd": (_c_int, [ctypes.POINTER(WAttnDesc)] + [_vp] * 16),

@@ -989,14 +989,15 @@ class _SplitKLinear(torch.autograd.Function):
     GEMM tiles only the output and runs a few dozen workgroups (57-114 us a call, profiles/).
     Under bf16 autocast the products run in bf16 like F.linear's; the gradients come back in the
     parameters' own dtype.  The autocast casts of x and W are made once, in the forward, and the bf16
-    copies are what the backward keeps (no re-cast per backward), and the fp32 sums of dW's chunks
-    and of db read the bf16 values directly (sum with dtype=float32: no cast pass)."""
+    copies are what the backward keeps (no re-cast per backward).  On the device the chunk-order
+    sum of dW's partials and the column sums of db run in one HIP launch pair reading the bf16
+    values directly (mmni_splitk_reduce; torch's two reductions took 24 us per Linear at C5)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.x_dtype = x.dtype
         if torch.is_autocast_enabled() and x.is_cuda:
-            cdt = torch.get_autocast_gpu_dtype()
+            cdt = torch.get_autocast_dtype("cuda")
             xc, wc = x.to(cdt), weight.to(cdt)
             bc = bias.to(cdt) if bias is not None else None
             with torch.autocast(device_type="cuda", enabled=False):
@@ -1020,8 +1021,14 @@ class _SplitKLinear(torch.autograd.Function):
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K).to(cdt)
         rows = dy2.shape[0]
-        acc = torch.promote_types(cdt, torch.float32)   # fp32 sums (fp64 stays fp64)
         S = _splitk_chunks(rows)
+        if dy.is_cuda and cdt in (torch.float32, torch.bfloat16):
+            dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+            db = torch.empty(N, device=dy.device, dtype=torch.float32) if ctx.has_bias else None
+            _splitk_wgrad(dy2, x2, dw, db)
+            return dx, dw.to(ctx.w_dtype), (db.to(ctx.w_dtype) if db is not None else None)
+        # CPU tensors (the float64 gradient tests): the same chunking in torch
+        acc = torch.promote_types(cdt, torch.float32)   # fp32 sums (fp64 stays fp64)
         if S > 1:
             r = rows // S
             dw = torch.bmm(dy2.view(S, r, N).transpose(1, 2), x2.view(S, r, K)).sum(0, dtype=acc)
@@ -1029,6 +1036,92 @@ class _SplitKLinear(torch.autograd.Function):
             dw = (dy2.t() @ x2).to(acc)
         db = dy2.sum(0, dtype=acc).to(ctx.w_dtype) if ctx.has_bias else None
         return dx, dw.to(ctx.w_dtype), db
+
+
+def _splitk_wgrad(dy2, x2, dw, db):
+    """dw (N, K) = dy2^T x2 and db (N) = colsum dy2 (nullable) into fp32 destinations (contiguous
+    row blocks of a larger gradient are fine): the S chunk products on the library GEMM, their
+    chunk-order sum and db in one HIP launch pair (mmni_splitk_reduce, splitk.hip)."""
+    rows, N = dy2.shape
+    K = x2.shape[1]
+    S = _splitk_chunks(rows)
+    if S > 1:
+        r = rows // S
+        part = torch.bmm(dy2.view(S, r, N).transpose(1, 2), x2.view(S, r, K))
+    else:
+        part = dy2.t() @ x2
+    dy2 = dy2.contiguous()
+    L = _lib.load()
+    ws = _workspace(L.mmni_splitk_reduce_workspace_bytes(rows, N), dy2.device) if db is not None else None
+    ev = KernelTimer.start()
+    check(L.mmni_splitk_reduce(S, N * K, ptr(part.contiguous()), rows, N, ptr(dy2), N,
+                               1 if dy2.dtype == torch.bfloat16 else 0, ptr(dw), ptr(db), ptr(ws),
+                               stream_handle(dy2.device)), "mmni_splitk_reduce")
+    KernelTimer.stop(f"splitk_reduce_{N}x{K}", ev, float(S * N * K + rows * N),
+                     float(part.element_size() * (S * N * K + rows * N) + 4 * (N * K + N)))
+
+
+class _InProjQKV(torch.autograd.Function):
+    """The cross-attention in_proj of MultiheadAttention (multihead_attention.py:71-84 in_proj_q /
+    in_proj_kv on one packed (3E, E) weight): q = x_q W[:E]^T + b[:E], kv = x_kv W[E:]^T + b[E:]
+    in one autograd node, so the weight and bias gradients are written as row blocks of one
+    (3E, E) / (3E) gradient (no zero-filled slice gradients and accumulation adds) and the autocast
+    casts of W and b happen once.  Weight gradients as _SplitKLinear (split-K, deterministic)."""
+
+    @staticmethod
+    def forward(ctx, xq, xkv, weight, bias):
+        E = weight.shape[1]
+        ctx.dtypes = (xq.dtype, xkv.dtype, weight.dtype)
+        if torch.is_autocast_enabled() and xq.is_cuda:
+            cdt = torch.get_autocast_dtype("cuda")
+            xq, xkv, wc = xq.to(cdt), xkv.to(cdt), weight.to(cdt)
+            bc = bias.to(cdt) if bias is not None else None
+        else:
+            wc, bc = weight, bias
+        with torch.autocast(device_type="cuda", enabled=False):
+            q = F.linear(xq, wc[:E], bc[:E] if bc is not None else None)
+            kv = F.linear(xkv, wc[E:], bc[E:] if bc is not None else None)
+        ctx.save_for_backward(xq, xkv, wc)
+        ctx.has_bias = bias is not None
+        return q, kv
+
+    @staticmethod
+    def backward(ctx, dq, dkv):
+        xq, xkv, wc = ctx.saved_tensors
+        xq_dtype, xkv_dtype, w_dtype = ctx.dtypes
+        E = wc.shape[1]
+        cdt = wc.dtype
+        dq = dq.to(cdt)
+        dkv = dkv.to(cdt)
+        dxq = (dq @ wc[:E]).to(xq_dtype) if ctx.needs_input_grad[0] else None
+        dxkv = (dkv @ wc[E:]).to(xkv_dtype) if ctx.needs_input_grad[1] else None
+        dw = torch.empty(3 * E, E, device=wc.device, dtype=torch.float32)
+        db = torch.empty(3 * E, device=wc.device, dtype=torch.float32) if ctx.has_bias else None
+        _splitk_wgrad(dq.reshape(-1, E), xq.reshape(-1, E), dw[:E], db[:E] if db is not None else None)
+        _splitk_wgrad(dkv.reshape(-1, 2 * E), xkv.reshape(-1, E), dw[E:], db[E:] if db is not None else None)
+        return dxq, dxkv, dw.to(w_dtype), (db.to(w_dtype) if db is not None else None)
+
+
+def in_proj_q_kv(xq, xkv, weight, bias=None):
+    """(q, kv) = the cross-attention in_proj of one packed weight (see _InProjQKV); device only."""
+    require_device(xq, xkv, weight, bias, what="in_proj_q_kv", dtypes=(torch.float32, torch.bfloat16))
+    return _InProjQKV.apply(xq, xkv, weight, bias)
+
+
+def mha_packed(q_src, kv_src, heads, causal_diag=0, scale=None, dropout=0.0, seed=None):
+    """The attention core on packed projections (T, B, 3E) qkv (kv_src None: self attention) or
+    (Tq, B, E) q + (Tk, B, 2E) kv: no slice copies forward, packed gradients backward (_MHARows).
+    Returns the (Tq, B, E) output in the projections' dtype."""
+    Tq, B = q_src.shape[0], q_src.shape[1]
+    E = q_src.shape[-1] // 3 if kv_src is None else q_src.shape[-1]
+    if scale is None:
+        scale = (E // heads) ** -0.5
+    if dropout > 0 and seed is None:
+        seed = dropout_seed()
+    q2 = _rows_view(q_src, q_src.shape[-1])
+    kv2 = q2 if kv_src is None else _rows_view(kv_src, kv_src.shape[-1])
+    Tk = Tq if kv_src is None else kv_src.shape[0]
+    return _MHARows.apply(q2, kv2, Tq, Tk, B, heads, causal_diag, scale, float(dropout), int(seed or 0))
 
 
 def splitk_linear(x, weight, bias=None):
@@ -1305,10 +1398,14 @@ class _MHARows(torch.autograd.Function):
     """The fused attention core on projections that stay packed: self attention reads q / k / v as
     column slices of one (T*B, 3E) qkv tensor, cross attention q (T*B, E) and k / v as slices of a
     (Tk*B, 2E) kv tensor; the backward writes dq / dk / dv straight into the packed gradients
-    (the kernels take row strides), so no slice copies or gradient scatter run in between."""
+    (the kernels take row strides), so no slice copies or gradient scatter run in between.  fp32 or
+    bf16 storage (the output and gradients follow it)."""
 
     @staticmethod
     def forward(ctx, q_src, kv_src, Tq, Tk, B, heads, diag, scale, dropout, seed):
+        require_device(q_src, kv_src, what="mha", dtypes=(torch.float32, torch.bfloat16))
+        if q_src.dtype != kv_src.dtype:
+            raise RuntimeError(f"mha: q / kv dtypes differ ({q_src.dtype}, {kv_src.dtype})")
         packed = q_src is kv_src
         E = q_src.shape[-1] // 3 if packed else q_src.shape[-1]
         qs = q_src.stride(0)
@@ -1318,15 +1415,18 @@ class _MHARows(torch.autograd.Function):
         else:
             q, k, v = q_src, kv_src, kv_src[:, E:]
             ks = vs = kv_src.stride(0)
-        out = torch.empty((Tq, B, E), device=q_src.device, dtype=torch.float32)
+        dt = q_src.dtype
+        out = torch.empty((Tq, B, E), device=q_src.device, dtype=dt)
         lse = torch.empty((B, heads, Tq), device=q_src.device, dtype=torch.float32)
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed)
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed, dt)
         lib = _lib.load()
         ws = _workspace(lib.mmni_mha_fwd_workspace_bytes(d), q_src.device)
         ev = KernelTimer.start()
         check(lib.mmni_mha_fwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(lse), ptr(ws), stream_handle(q_src.device)),
               "mmni_mha_fwd")
-        KernelTimer.stop(f"mha_fwd_E{E}", ev, 4.0 * Tq * Tk * B * E, 4.0 * B * E * (2 * Tq + 2 * Tk))
+        sfx = "_bf16" if dt == torch.bfloat16 else ""
+        KernelTimer.stop(f"mha_fwd_E{E}{sfx}", ev, 4.0 * Tq * Tk * B * E,
+                         q_src.element_size() * B * E * (2 * Tq + 2 * Tk))
         ctx.save_for_backward(q_src, kv_src, out, lse)
         ctx.cfg = (Tq, Tk, B, heads, diag, scale, dropout, seed, packed, E, qs, ks, vs)
         return out
@@ -1335,7 +1435,7 @@ class _MHARows(torch.autograd.Function):
     def backward(ctx, dout):
         q_src, kv_src, out, lse = ctx.saved_tensors
         Tq, Tk, B, heads, diag, scale, dropout, seed, packed, E, qs, ks, vs = ctx.cfg
-        dout = dout.contiguous()
+        dout = dout.contiguous().to(q_src.dtype)
         dq_src = torch.empty_like(q_src)
         if packed:
             q, k, v = q_src, q_src[:, E:], q_src[:, 2 * E:]
@@ -1345,13 +1445,16 @@ class _MHARows(torch.autograd.Function):
             dkv_src = torch.empty_like(kv_src)
             q, k, v = q_src, kv_src, kv_src[:, E:]
             dq, dk, dv = dq_src, dkv_src, dkv_src[:, E:]
-        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed)
+        dt = q_src.dtype
+        d = _mha_desc(Tq, Tk, B, heads, E // heads, diag, scale, qs, ks, vs, E, dropout, seed, dt)
         lib = _lib.load()
         ws = _workspace(lib.mmni_mha_bwd_workspace_bytes(d), q_src.device)
         ev = KernelTimer.start()
         check(lib.mmni_mha_bwd(d, ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv),
                                ptr(ws), stream_handle(q_src.device)), "mmni_mha_bwd")
-        KernelTimer.stop(f"mha_bwd_E{E}", ev, 10.0 * Tq * Tk * B * E, 4.0 * B * E * (4 * Tq + 4 * Tk))
+        sfx = "_bf16" if dt == torch.bfloat16 else ""
+        KernelTimer.stop(f"mha_bwd_E{E}{sfx}", ev, 10.0 * Tq * Tk * B * E,
+                         q_src.element_size() * B * E * (4 * Tq + 4 * Tk))
         return dq_src, dkv_src, None, None, None, None, None, None, None, None
 
 

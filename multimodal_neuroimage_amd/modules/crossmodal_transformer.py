@@ -106,8 +106,12 @@ class TransformerEncoderLayer(nn.Module):
         if x_k is None and x_v is None:
             x, _ = self.self_attn(query=x, key=x, value=x, attn_mask=mask, need_weights=False)
         else:
+            # one LayerNorm when key and value are one tensor (the encoder's shared embedding): the
+            # two normalised copies are equal, and one tensor lets the attention project k and v in
+            # one GEMM and keep them packed
+            same = x_k is x_v
             x_k = self.maybe_layer_norm(0, x_k, before=True)
-            x_v = self.maybe_layer_norm(0, x_v, before=True)
+            x_v = x_k if same else self.maybe_layer_norm(0, x_v, before=True)
             x, _ = self.self_attn(query=x, key=x_k, value=x_v, attn_mask=mask, need_weights=False)
         x = F.dropout(x, p=self.res_dropout, training=self.training)
         x = residual + x

@@ -18,7 +18,8 @@ from torch import nn
 from torch.nn import Parameter
 import torch.nn.functional as F
 
-from ..functional import SplitKLinear, dropout_seed, mha_core, mha_mean_probs, splitk_linear
+from ..functional import (SplitKLinear, dropout_seed, in_proj_q_kv, mha_core, mha_mean_probs, mha_packed,
+                          splitk_linear)
 
 
 def causal_diag_of(attn_mask, Tq, Tk):
@@ -82,6 +83,18 @@ class MultiheadAttention(nn.Module):
         assert key.size() == value.size()
         src_len = key.size(0)
         diag = causal_diag_of(attn_mask, tgt_len, src_len)
+        p = float(self.attn_dropout) if self.training else 0.0
+        if not need_weights and query.is_cuda and key.data_ptr() == value.data_ptr():
+            # packed projections straight into the attention core: self attention on one qkv GEMM,
+            # cross attention on q + one kv GEMM of the packed weight (one autograd node, row-block
+            # weight gradients); k / v stay column slices and their gradients arrive packed
+            seed = dropout_seed() if p > 0 else 0
+            if query.data_ptr() == key.data_ptr():
+                attn = mha_packed(self._in_proj(query), None, self.num_heads_mult, diag, self.scaling, p, seed)
+            else:
+                q, kv = in_proj_q_kv(query, key, self.in_proj_weight, self.in_proj_bias)
+                attn = mha_packed(q, kv, self.num_heads_mult, diag, self.scaling, p, seed)
+            return self.out_proj(attn), None
         if query.data_ptr() == key.data_ptr() == value.data_ptr():
             q, k, v = self._in_proj(query).chunk(3, dim=-1)
         elif key.data_ptr() == value.data_ptr():
@@ -91,7 +104,6 @@ class MultiheadAttention(nn.Module):
             q = self._in_proj(query, end=self.embed_dim)
             k = self._in_proj(key, start=self.embed_dim, end=2 * self.embed_dim)
             v = self._in_proj(value, start=2 * self.embed_dim)
-        p = float(self.attn_dropout) if self.training else 0.0
         seed = dropout_seed() if p > 0 else 0
         attn, lse = mha_core(q, k, v, self.num_heads_mult, diag, self.scaling, dropout=p, seed=seed)
         attn = self.out_proj(attn)
@@ -116,8 +128,10 @@ class MultiheadAttention(nn.Module):
         return self._in_proj(value, start=2 * self.embed_dim)
 
     def _in_proj(self, input, start=0, end=None, **kwargs):
-        weight = kwargs.get('weight', self.in_proj_weight)[start:end, :]
+        weight = kwargs.get('weight', self.in_proj_weight)
         bias = kwargs.get('bias', self.in_proj_bias)
-        if bias is not None:
-            bias = bias[start:end]
+        if start != 0 or end is not None:   # whole-weight projections stay unsliced (no slice gradient)
+            weight = weight[start:end, :]
+            if bias is not None:
+                bias = bias[start:end]
         return splitk_linear(input, weight, bias)

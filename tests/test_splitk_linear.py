@@ -66,3 +66,30 @@ def test_bf16_autocast_matches_f_linear():
         for a, r in zip(got, ref):
             err = float((a - r).abs().max() / r.abs().max())
             assert err < 2e-2, err
+
+
+@pytest.mark.gpu
+def test_device_reduction_fp32_matches_float64():
+    """fp32 on the device (mmni_splitk_reduce for the chunk sum and db): gradients against float64
+    autograd, for a split (6,912 rows: S = 27), an unsplit odd-width case and no bias; two runs are
+    bitwise equal (fixed-order sums)."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(1)
+    for rows_shape, N, K, bias in (((1728, 4), 84, 252, True), ((77, 3), 13, 84, True), ((512, 8), 168, 84, False)):
+        x = torch.randn(*rows_shape, K, generator=g, dtype=torch.float64)
+        w = torch.randn(N, K, generator=g, dtype=torch.float64) * 0.1
+        b = torch.randn(N, generator=g, dtype=torch.float64) if bias else None
+        gy = torch.randn(*rows_shape, N, generator=g, dtype=torch.float64)
+        ref = []
+        leaves = [t.clone().requires_grad_(True) if t is not None else None for t in (x, w, b)]
+        (torch.nn.functional.linear(*leaves) * gy).sum().backward()
+        ref = [t.grad for t in leaves if t is not None]
+        runs = []
+        for _ in range(2):
+            lv = [t.float().to(dev).requires_grad_(True) if t is not None else None for t in (x, w, b)]
+            splitk_linear(*lv).backward(gy.float().to(dev))
+            runs.append([t.grad.clone() for t in lv if t is not None])
+        for a, a2, r in zip(runs[0], runs[1], ref):
+            assert torch.equal(a, a2)
+            err = float((a.double().cpu() - r).abs().max() / r.abs().max())
+            assert err < 1e-5, err
