@@ -375,6 +375,16 @@ int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn,
                            const float* gamma, const float* mean, const float* rstd, const float* dres,
                            int64_t ldres, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace,
                            void* stream);
+/* ABI v8: the same two with the LayerNorm output y (fwd) / input gradient dxn (bwd) stored as fp32
+ * (dtype 0) or bf16 (dtype 1): the bf16 crossmodal head's pre-norms feed bf16 GEMMs directly
+ * (torch autocast computes layer_norm in fp32 and the consuming Linear rounds it to bf16; the
+ * kernel rounds the same fp32 value once). */
+int mmni_row_layernorm_fwd_t(int64_t rows, int C, const float* x, int64_t ldx, const float* gamma, const float* beta,
+                             float eps, void* y, int y_dtype, int64_t ldy, float* mean, float* rstd, void* stream);
+int mmni_row_layernorm_bwd_t(int64_t rows, int C, const void* dxn, int dxn_dtype, int64_t lddxn, const float* x,
+                             int64_t ldx, const float* gamma, const float* mean, const float* rstd, const float* dres,
+                             int64_t ldres, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace,
+                             void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Split-K weight-gradient reductions (ABI v8) of the crossmodal encoder's Linears

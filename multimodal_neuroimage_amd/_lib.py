@@ -78,6 +78,10 @@ SIGNATURES = {
     "mmni_row_layernorm_fwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _vp, ctypes.c_float, _vp, _c_i64, _vp, _vp,
                                         _vp]),
     "mmni_row_layernorm_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
+    "mmni_row_layernorm_fwd_t": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _vp, ctypes.c_float, _vp, _c_int, _c_i64,
+                                          _vp, _vp, _vp]),
+    "mmni_row_layernorm_bwd_t": (_c_int, [_c_i64, _c_int, _vp, _c_int, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
+                                          _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "mmni_cpb_fwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 6),
     "mmni_cpb_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int, _c_int, _c_int]),
     "mmni_cpb_bwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 11),

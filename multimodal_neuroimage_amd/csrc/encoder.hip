@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict_
 struct LNBArgs {
     int64_t rows, lddxn, ldx, ldres, lddx;
     int C;
-    const float* dxn;
+    const void* dxn;   // float, or __bf16 (the bf16 head's linears hand back bf16 input gradients)
     const float* x;
     const float* gamma;
     const float* mean;
@@ -489,9 +489,13 @@ struct LNBArgs {
     float* part;   // [block][2C]: dgamma | dbeta
 };
 
-template <bool RES>
+template <typename TI>
+__device__ __forceinline__ float ln_ld(const TI* p) { return (float)*p; }
+
+template <bool RES, typename TI = float>
 __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
     __shared__ float red[4][2][256];
+    const TI* dxn = static_cast<const TI*>(a.dxn);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f}, gm[4];
     int cc[4];
@@ -507,7 +511,7 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
         float d[4], xv[4], rv[4], xh[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            d[j] = a.dxn[r * a.lddxn + cc[j]];
+            d[j] = ln_ld<TI>(dxn + r * a.lddxn + cc[j]);
             xv[j] = a.x[r * a.ldx + cc[j]];
             rv[j] = RES ? a.dres[r * a.ldres + cc[j]] : 0.f;
         }
@@ -550,9 +554,10 @@ __global__ __launch_bounds__(256) void row_ln_bwd_kernel(LNBArgs a) {
 
 // LayerNorm forward on rows of C <= 256: a wave per row, 4 columns per lane (two butterfly sums:
 // mean, then the centred second moment); (mean, rstd) written for the backward.
+template <typename TO = float>
 __global__ __launch_bounds__(256) void row_ln_fwd_kernel(int64_t rows, int C, const float* __restrict__ x,
                                                          int64_t ldx, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float eps, float* y,
+                                                         const float* __restrict__ beta, float eps, TO* y,
                                                          int64_t ldy, float* mean, float* rstd) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float gm[4], bt[4];
@@ -585,7 +590,7 @@ __global__ __launch_bounds__(256) void row_ln_fwd_kernel(int64_t rows, int C, co
         const float rs = 1.0f / sqrtf(q * invC + eps);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (in[j]) y[r * ldy + lane + 64 * j] = fmaf((v[j] - mu) * rs, gm[j], bt[j]);
+            if (in[j]) y[r * ldy + lane + 64 * j] = (TO)fmaf((v[j] - mu) * rs, gm[j], bt[j]);
         if (lane == 0) {
             mean[r] = mu;
             rstd[r] = rs;
@@ -711,14 +716,26 @@ size_t enc_row_ln_bwd_workspace(int64_t rows, int C) {
 int enc_row_ln_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
                    const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
                    float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s) {
+    return enc_row_ln_bwd_t(rows, C, dxn, 0, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma, dbeta,
+                            workspace, s);
+}
+
+int enc_row_ln_bwd_t(int64_t rows, int C, const void* dxn, int dxn_bf16, int64_t lddxn, const float* x, int64_t ldx,
+                     const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                     float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s) {
     enc::LNBArgs a{};
     a.rows = rows; a.lddxn = lddxn; a.ldx = ldx; a.ldres = ldres; a.lddx = lddx; a.C = C;
     a.dxn = dxn; a.x = x; a.gamma = gamma; a.mean = mean; a.rstd = rstd; a.dres = dres; a.dx = dx;
     a.part = static_cast<float*>(workspace);
     int64_t blocks = (rows + 3) / 4;
     if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
-    if (dres != nullptr) enc::row_ln_bwd_kernel<true><<<(unsigned)blocks, 256, 0, s>>>(a);
-    else enc::row_ln_bwd_kernel<false><<<(unsigned)blocks, 256, 0, s>>>(a);
+    if (dxn_bf16) {
+        if (dres != nullptr) enc::row_ln_bwd_kernel<true, __bf16><<<(unsigned)blocks, 256, 0, s>>>(a);
+        else enc::row_ln_bwd_kernel<false, __bf16><<<(unsigned)blocks, 256, 0, s>>>(a);
+    } else {
+        if (dres != nullptr) enc::row_ln_bwd_kernel<true><<<(unsigned)blocks, 256, 0, s>>>(a);
+        else enc::row_ln_bwd_kernel<false><<<(unsigned)blocks, 256, 0, s>>>(a);
+    }
     int rc = launch_status("row_layernorm_bwd");
     if (rc) return rc;
     enc::chunk_sum(a.part, (int)blocks, 2 * C, C, dgamma, dbeta, s);
@@ -751,24 +768,45 @@ extern "C" int mmni_row_layernorm_bwd(int64_t rows, int C, const float* dxn, int
                                       int64_t ldx, const float* gamma, const float* mean, const float* rstd,
                                       const float* dres, int64_t ldres, float* dx, int64_t lddx, float* dgamma,
                                       float* dbeta, void* workspace, void* stream) {
+    return mmni_row_layernorm_bwd_t(rows, C, dxn, 0, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma,
+                                    dbeta, workspace, stream);
+}
+
+extern "C" int mmni_row_layernorm_bwd_t(int64_t rows, int C, const void* dxn, int dxn_dtype, int64_t lddxn,
+                                        const float* x, int64_t ldx, const float* gamma, const float* mean,
+                                        const float* rstd, const float* dres, int64_t ldres, float* dx, int64_t lddx,
+                                        float* dgamma, float* dbeta, void* workspace, void* stream) {
     MMNI_ARG_CHECK(dxn && x && gamma && mean && rstd && dx && dgamma && dbeta && workspace,
                    "row_layernorm_bwd: null pointer");
     MMNI_ARG_CHECK(rows > 0 && C > 0 && C <= 256, "row_layernorm_bwd: C=%d outside 1..256", C);
     MMNI_ARG_CHECK(lddxn >= C && ldx >= C && lddx >= C && (dres == nullptr || ldres >= C),
                    "row_layernorm_bwd: leading dimensions below C");
-    return enc_row_ln_bwd(rows, C, dxn, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma, dbeta,
-                          workspace, (hipStream_t)stream);
+    MMNI_ARG_CHECK(dxn_dtype == 0 || dxn_dtype == 1, "row_layernorm_bwd: dxn dtype %d (0 fp32, 1 bf16)", dxn_dtype);
+    return enc_row_ln_bwd_t(rows, C, dxn, dxn_dtype, lddxn, x, ldx, gamma, mean, rstd, dres, ldres, dx, lddx, dgamma,
+                            dbeta, workspace, (hipStream_t)stream);
 }
 
 extern "C" int mmni_row_layernorm_fwd(int64_t rows, int C, const float* x, int64_t ldx, const float* gamma,
                                       const float* beta, float eps, float* y, int64_t ldy, float* mean, float* rstd,
                                       void* stream) {
+    return mmni_row_layernorm_fwd_t(rows, C, x, ldx, gamma, beta, eps, y, 0, ldy, mean, rstd, stream);
+}
+
+extern "C" int mmni_row_layernorm_fwd_t(int64_t rows, int C, const float* x, int64_t ldx, const float* gamma,
+                                        const float* beta, float eps, void* y, int y_dtype, int64_t ldy, float* mean,
+                                        float* rstd, void* stream) {
     MMNI_ARG_CHECK(x && gamma && beta && y && mean && rstd, "row_layernorm_fwd: null pointer");
     MMNI_ARG_CHECK(rows > 0 && C > 0 && C <= 256, "row_layernorm_fwd: C=%d outside 1..256", C);
     MMNI_ARG_CHECK(ldx >= C && ldy >= C, "row_layernorm_fwd: leading dimensions below C");
+    MMNI_ARG_CHECK(y_dtype == 0 || y_dtype == 1, "row_layernorm_fwd: y dtype %d (0 fp32, 1 bf16)", y_dtype);
     int64_t blocks = (rows + 7) / 8;   // ~2 rows per wave
     if (blocks > 4096) blocks = 4096;
-    enc::row_ln_fwd_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(rows, C, x, ldx, gamma, beta, eps, y,
-                                                                             ldy, mean, rstd);
+    hipStream_t s = (hipStream_t)stream;
+    if (y_dtype == 1)
+        enc::row_ln_fwd_kernel<__bf16><<<(unsigned)blocks, 256, 0, s>>>(rows, C, x, ldx, gamma, beta, eps,
+                                                                         static_cast<__bf16*>(y), ldy, mean, rstd);
+    else
+        enc::row_ln_fwd_kernel<float><<<(unsigned)blocks, 256, 0, s>>>(rows, C, x, ldx, gamma, beta, eps,
+                                                                        static_cast<float*>(y), ldy, mean, rstd);
     return launch_status("row_layernorm_fwd");
 }

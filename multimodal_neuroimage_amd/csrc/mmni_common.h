@@ -63,6 +63,10 @@ size_t enc_row_ln_bwd_workspace(int64_t rows, int C);
 int enc_row_ln_bwd(int64_t rows, int C, const float* dxn, int64_t lddxn, const float* x, int64_t ldx,
                    const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
                    float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s);
+// the same with the input gradient dxn in fp32 (dxn_bf16 = 0) or bf16 (1)
+int enc_row_ln_bwd_t(int64_t rows, int C, const void* dxn, int dxn_bf16, int64_t lddxn, const float* x, int64_t ldx,
+                     const float* gamma, const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                     float* dx, int64_t lddx, float* dgamma, float* dbeta, void* workspace, hipStream_t s);
 constexpr int64_t kSmallRows = 65536;   // token ops at or below this row count take the encoder kernels
 
 }  // namespace mmni

@@ -515,22 +515,24 @@ class _LayerNorm(torch.autograd.Function):
 
 class _RowLayerNorm(torch.autograd.Function):
     """nn.LayerNorm over rows of C <= 256 (the crossmodal encoder's 84 / 168) on the wave-per-row
-    kernels (mmni_row_layernorm_fwd / _bwd).  Computes in fp32 and returns fp32 — what torch's
-    autocast does with layer_norm — from fp32 or bf16 input; the input gradient comes back in the
+    kernels (mmni_row_layernorm_fwd_t / _bwd_t).  Computes in fp32 and returns fp32 — what torch's
+    autocast does with layer_norm — from fp32 or bf16 input; out_dtype=bf16 stores the output
+    rounded to bf16 for a consumer that is a bf16 GEMM (the autocast Linear would round the fp32
+    output the same way), and then takes its gradient in bf16.  The input gradient comes back in the
     input's dtype."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, out_dtype):
         C = x.shape[-1]
         x2 = x.reshape(-1, C).float().contiguous()
         w, b = weight.float().contiguous(), bias.float().contiguous()
         rows = x2.shape[0]
-        y = torch.empty_like(x2)
+        y = torch.empty(x2.shape, device=x.device, dtype=out_dtype)
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
-        check(_lib.load().mmni_row_layernorm_fwd(rows, C, ptr(x2), C, ptr(w), ptr(b), float(eps), ptr(y), C,
-                                                 ptr(mean), ptr(rstd), stream_handle(x.device)),
-              "mmni_row_layernorm_fwd")
+        check(_lib.load().mmni_row_layernorm_fwd_t(rows, C, ptr(x2), C, ptr(w), ptr(b), float(eps), ptr(y),
+                                                   1 if out_dtype == torch.bfloat16 else 0, C, ptr(mean), ptr(rstd),
+                                                   stream_handle(x.device)), "mmni_row_layernorm_fwd")
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.shape, ctx.dtype, ctx.wdtype = x.shape, x.dtype, weight.dtype
         return y.view(x.shape)
@@ -538,21 +540,26 @@ class _RowLayerNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
-        dx, dg, db = row_layernorm_bwd(dy.reshape(x2.shape).float().contiguous(), x2, w, mean, rstd)
-        return dx.view(ctx.shape).to(ctx.dtype), dg.to(ctx.wdtype), db.to(ctx.wdtype), None
+        dy2 = dy.reshape(x2.shape)
+        if dy2.dtype not in (torch.float32, torch.bfloat16):
+            dy2 = dy2.float()
+        dx, dg, db = row_layernorm_bwd(dy2.contiguous(), x2, w, mean, rstd)
+        return dx.view(ctx.shape).to(ctx.dtype), dg.to(ctx.wdtype), db.to(ctx.wdtype), None, None
 
 
-def layer_norm(x, ln):
+def layer_norm(x, ln, out_dtype=None):
     """nn.LayerNorm `ln` applied to x (..., C) with the HIP kernels: the token kernels at C in
     12/24/48/96, the wave-per-row kernels up to C = 256 (the crossmodal stack's 84/168), torch's
-    ROCm LayerNorm beyond.  No CPU path."""
+    ROCm LayerNorm beyond.  out_dtype=torch.bfloat16 (row kernels only) stores the output in bf16 for
+    a bf16 GEMM consumer.  No CPU path."""
     require_device(x, what="layer_norm", dtypes=(torch.float32, torch.bfloat16))
     C = x.shape[-1]
-    if C in LN_CHANNELS and x.dtype == torch.float32:
+    if C in LN_CHANNELS and x.dtype == torch.float32 and out_dtype is None:
         return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
     if C <= 256 and ln.elementwise_affine and ln.bias is not None:
-        return _RowLayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
-    return ln(x)
+        return _RowLayerNorm.apply(x, ln.weight, ln.bias, ln.eps, out_dtype or torch.float32)
+    y = ln(x)
+    return y.to(out_dtype) if out_dtype is not None else y
 
 
 _DW_TILES = {(1, 1), (1, 2), (1, 3), (2, 1), (3, 1), (2, 2), (3, 3), (1, 4), (4, 1), (2, 3), (3, 2), (9, 3), (3, 9),
@@ -1266,10 +1273,10 @@ def row_layernorm_bwd(dxn2, x2, gamma, mean, rstd, dres2=None):
     L = _lib.load()
     ws = _workspace(L.mmni_row_layernorm_bwd_workspace_bytes(rows, C), x2.device)
     ev = KernelTimer.start()
-    check(L.mmni_row_layernorm_bwd(rows, C, ptr(dxn2), dxn2.stride(0), ptr(x2), x2.stride(0), ptr(gamma), ptr(mean),
-                                   ptr(rstd), ptr(dres2), dres2.stride(0) if dres2 is not None else 0, ptr(dx), C,
-                                   ptr(dgamma), ptr(dbeta), ptr(ws), stream_handle(x2.device)),
-          "mmni_row_layernorm_bwd")
+    check(L.mmni_row_layernorm_bwd_t(rows, C, ptr(dxn2), 1 if dxn2.dtype == torch.bfloat16 else 0, dxn2.stride(0),
+                                     ptr(x2), x2.stride(0), ptr(gamma), ptr(mean), ptr(rstd), ptr(dres2),
+                                     dres2.stride(0) if dres2 is not None else 0, ptr(dx), C, ptr(dgamma), ptr(dbeta),
+                                     ptr(ws), stream_handle(x2.device)), "mmni_row_layernorm_bwd")
     KernelTimer.stop(f"row_ln_bwd_C{C}", ev, 10.0 * rows * C, 4.0 * rows * C * (4 if dres2 is not None else 3))
     return dx, dgamma, dbeta
 

@@ -129,7 +129,12 @@ class TransformerEncoderLayer(nn.Module):
         assert before ^ after
         if not (after ^ self.normalize_before):
             return x
-        return layer_norm(x, self.layer_norms[i]) if x.is_cuda else self.layer_norms[i](x)
+        if not x.is_cuda:
+            return self.layer_norms[i](x)
+        # a pre-norm feeds only the layer's Linears: under autocast its output is stored in the
+        # GEMMs' dtype (no separate cast pass; same rounding as the autocast Linear's)
+        out = torch.get_autocast_dtype("cuda") if (before and torch.is_autocast_enabled()) else None
+        return layer_norm(x, self.layer_norms[i], out)
 
 
 def fill_with_neg_inf(t):

@@ -190,3 +190,29 @@ def test_row_layernorm_module_vs_fp64(device, rows, C, dtype):
     assert rel_err(y, yd) < 1e-5
     assert rel_err(x.grad.float(), xd.grad) < tol
     assert rel_err(ln.weight.grad, wd.grad) < 1e-5 and rel_err(ln.bias.grad, bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("rows,C", [(4096 * 8, 84), (777, 168), (50, 200)])
+def test_row_layernorm_bf16_output_vs_fp64(device, rows, C):
+    """out_dtype=bf16 (the bf16 head's pre-norms, mmni_row_layernorm_fwd_t / _bwd_t): the output is the
+    fp32 LayerNorm rounded once to bf16 (bit-equal to rounding the fp32 kernel's output), and a bf16
+    output gradient gives the input / affine gradients of float64 autograd fed the same bf16 values."""
+    ln = torch.nn.LayerNorm(C).to(device)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.normal_()
+    g = torch.Generator(device=device).manual_seed(rows * 3 + C)
+    x = (torch.randn(rows, C, device=device, generator=g) * 2 + 1).requires_grad_(True)
+    gy = torch.randn(rows, C, device=device, generator=g).to(torch.bfloat16)
+    y = MF.layer_norm(x, ln, torch.bfloat16)
+    assert y.dtype == torch.bfloat16
+    with torch.no_grad():
+        y32 = MF.layer_norm(x, ln)
+    assert torch.equal(y, y32.to(torch.bfloat16))
+    y.backward(gy)
+    xd = x.detach().double().requires_grad_(True)
+    wd, bd = ln.weight.detach().double().requires_grad_(True), ln.bias.detach().double().requires_grad_(True)
+    torch.nn.functional.layer_norm(xd, (C,), wd, bd, ln.eps).backward(gy.double())
+    assert x.grad.dtype == torch.float32
+    assert rel_err(x.grad, xd.grad) < 1e-5
+    assert rel_err(ln.weight.grad, wd.grad) < 1e-5 and rel_err(ln.bias.grad, bd.grad) < 1e-5
