@@ -396,6 +396,11 @@ int mmni_row_layernorm_bwd_t(int64_t rows, int C, const void* dxn, int dxn_dtype
  * part and dy are fp32 (dtype 0) or bf16 (dtype 1, the autocast head); sums and outputs fp32.
  * Bitwise deterministic.  Workspace: mmni_splitk_reduce_workspace_bytes(rows, N).
  * ------------------------------------------------------------------------------------ */
+#define MMNI_CAST_MAX_SEGS 64
+/* dst[i][e] = bf16(src[i][e]) (round to nearest even) for e < count[i], i < n <= 64, in one launch:
+ * the per-step bf16 copies of the head's Linear weights and biases under autocast (torch casts each
+ * one separately: ~8 launches per encoder layer).  src / dst / count are host arrays. */
+int mmni_cast_bf16_multi(int n, const float* const* src, void* const* dst, const int64_t* count, void* stream);
 size_t mmni_splitk_reduce_workspace_bytes(int64_t rows, int N);
 int mmni_splitk_reduce(int S, int64_t NK, const void* part, int64_t rows, int N, const void* dy, int64_t ldy,
                        int dtype, float* dw, float* db, void* workspace, void* stream);

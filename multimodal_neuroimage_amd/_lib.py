@@ -87,6 +87,7 @@ SIGNATURES = {
     "mmni_cpb_bwd": (_c_int, [_c_i64, _c_int, _c_int, _c_int] + [_vp] * 11),
     "mmni_row_layernorm_bwd": (_c_int, [_c_i64, _c_int, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp,
                                         _c_i64, _vp, _vp, _vp, _vp]),
+    "mmni_cast_bf16_multi": (_c_int, [_c_int, _vp, _vp, _vp, _vp]),
     "mmni_splitk_reduce_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_int]),
     "mmni_splitk_reduce": (_c_int, [_c_int, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
     "mmni_last_error": (ctypes.c_char_p, []),

@@ -425,23 +425,26 @@ __global__ __launch_bounds__(256) void rowgemm_dw_kernel(DWArgs a) {
 }
 
 // out[j] = sum_c part[c][j] (deterministic: fixed slices and a fixed tree); columns [0, split) ->
-// out, [split, ncols) -> out2 (nullable).  A block owns 32 columns (8 float4 quads) and splits the
-// chunks over 32 slices (slice s sums chunks s, s + 32, ... in order, 8 loads in flight), then adds
-// the slices by a fixed LDS tree.  One thread per column quad looping over 100+ chunks was a chain
-// of dependent load waits (~10 us per call).
-constexpr int kCsSlices = 32, kCsQuads = 8;
+// out, [split, ncols) -> out2 (nullable).  A block owns Q float4 column quads and splits the chunks
+// over SL = 256 / Q slices (slice s sums chunks s, s + SL, ... in order, 8 loads in flight), then
+// adds the slices by a fixed LDS tree.  Q = 8 for wide slabs (weight gradients); Q = 2 for narrow
+// ones (a LayerNorm's 2C dgamma | dbeta columns over 768 chunks: 6 blocks of 32 columns took
+// ~9.4 us a call, 21 blocks of 8 columns one load round).  One thread per column quad looping over
+// 100+ chunks was a chain of dependent load waits (~10 us per call).
+template <int Q>
 __global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ part, int nchunks, int ncols,
                                                         int split, float* out, float* out2) {
-    __shared__ f4 red[kCsSlices][kCsQuads];
-    const int q = threadIdx.x % kCsQuads, sl = threadIdx.x / kCsQuads;
-    const int j4 = (blockIdx.x * kCsQuads + q) * 4;
+    constexpr int SL = 256 / Q;
+    __shared__ f4 red[SL][Q];
+    const int q = threadIdx.x % Q, sl = threadIdx.x / Q;
+    const int j4 = (blockIdx.x * Q + q) * 4;
     const bool vec = (ncols & 3) == 0;
     f4 s = zero4();
-    for (int c0 = sl; c0 < nchunks; c0 += 8 * kCsSlices) {
+    for (int c0 = sl; c0 < nchunks; c0 += 8 * SL) {
         f4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int c = c0 + u * kCsSlices;
+            const int c = c0 + u * SL;
             const float* p = part + (int64_t)(c < nchunks ? c : nchunks - 1) * ncols;
             if (vec) {
                 v[u] = *reinterpret_cast<const f4*>(p + (j4 < ncols ? j4 : ncols - 4));
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict_
     red[sl][q] = s;
     __syncthreads();
 #pragma unroll
-    for (int h = kCsSlices / 2; h > 0; h >>= 1) {
+    for (int h = SL / 2; h > 0; h >>= 1) {
         if (sl < h) red[sl][q] += red[sl + h][q];
         __syncthreads();
     }
@@ -612,9 +615,11 @@ int dw_chunks(int64_t rows, int N, int K) {
 }
 
 void chunk_sum(const float* part, int nchunks, int ncols, int split, float* out, float* out2, hipStream_t s) {
-    const int cols_per_block = 4 * kCsQuads;
-    chunk_sum_kernel<<<(ncols + cols_per_block - 1) / cols_per_block, 256, 0, s>>>(part, nchunks, ncols, split, out,
-                                                                                  out2);
+    if (ncols <= 1024 && nchunks >= 256) {
+        chunk_sum_kernel<2><<<(ncols + 7) / 8, 256, 0, s>>>(part, nchunks, ncols, split, out, out2);
+    } else {
+        chunk_sum_kernel<8><<<(ncols + 31) / 32, 256, 0, s>>>(part, nchunks, ncols, split, out, out2);
+    }
 }
 
 }  // namespace enc

@@ -196,7 +196,56 @@ int64_t slab_rows(int64_t rows) {
 }  // namespace splitk
 }  // namespace mmni
 
+namespace mmni {
+namespace splitk {
+
+// fp32 -> bf16 (round to nearest even) of up to kMaxSegs tensors in one launch: blockIdx.y picks the
+// segment, blocks stride its elements 4 at a time
+struct CastSegs {
+    int n;
+    const float* src[MMNI_CAST_MAX_SEGS];
+    __bf16* dst[MMNI_CAST_MAX_SEGS];
+    int64_t count[MMNI_CAST_MAX_SEGS];
+};
+
+__global__ __launch_bounds__(kNT) void cast_bf16_kernel(CastSegs c) {
+    const int g = blockIdx.y;
+    const float* __restrict__ src = c.src[g];
+    __bf16* __restrict__ dst = c.dst[g];
+    const int64_t n = c.count[g];
+    for (int64_t e = ((int64_t)blockIdx.x * kNT + threadIdx.x) * 4; e < n; e += (int64_t)gridDim.x * kNT * 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (e + i < n) dst[e + i] = (__bf16)src[e + i];
+    }
+}
+
+}  // namespace splitk
+}  // namespace mmni
+
 using namespace mmni;
+
+extern "C" int mmni_cast_bf16_multi(int n, const float* const* src, void* const* dst, const int64_t* count,
+                                    void* stream) {
+    MMNI_ARG_CHECK(n >= 0 && n <= MMNI_CAST_MAX_SEGS && (n == 0 || (src && dst && count)),
+                   "cast_bf16_multi: %d segments (1..%d)", n, MMNI_CAST_MAX_SEGS);
+    if (n == 0) return 0;
+    splitk::CastSegs c{};
+    c.n = n;
+    int64_t mx = 0;
+    for (int i = 0; i < n; ++i) {
+        MMNI_ARG_CHECK(src[i] && dst[i] && count[i] >= 0, "cast_bf16_multi: segment %d", i);
+        c.src[i] = src[i];
+        c.dst[i] = static_cast<__bf16*>(dst[i]);
+        c.count[i] = count[i];
+        if (count[i] > mx) mx = count[i];
+    }
+    if (mx == 0) return 0;
+    int64_t bx = (mx + 4 * splitk::kNT - 1) / (4 * splitk::kNT);
+    if (bx > 64) bx = 64;
+    splitk::cast_bf16_kernel<<<dim3((unsigned)bx, (unsigned)n), splitk::kNT, 0, (hipStream_t)stream>>>(c);
+    return launch_status("cast_bf16_multi");
+}
 
 extern "C" size_t mmni_splitk_reduce_workspace_bytes(int64_t rows, int N) {
     if (rows <= 0 || N <= 0) return 0;

@@ -1005,8 +1005,8 @@ class _SplitKLinear(torch.autograd.Function):
         ctx.x_dtype = x.dtype
         if torch.is_autocast_enabled() and x.is_cuda:
             cdt = torch.get_autocast_dtype("cuda")
-            xc, wc = x.to(cdt), weight.to(cdt)
-            bc = bias.to(cdt) if bias is not None else None
+            xc, wc = x.to(cdt), _autocast_copy(weight, cdt)
+            bc = _autocast_copy(bias, cdt)
             with torch.autocast(device_type="cuda", enabled=False):
                 y = F.linear(xc, wc, bc)
         else:
@@ -1045,6 +1045,45 @@ class _SplitKLinear(torch.autograd.Function):
         return dx, dw.to(ctx.w_dtype), db
 
 
+# bf16 copies of fp32 parameters made for the current step (cast_params_bf16), looked up by the
+# autocast Linears instead of casting each weight and bias in its own launch
+_BF16_CACHE = {}
+
+
+def cast_params_bf16(params):
+    """bf16 copies of fp32 device parameters, up to 64 per HIP launch (mmni_cast_bf16_multi), kept
+    for this step's autocast Linears (_autocast_copy hands them out while the parameter's version
+    is unchanged; an optimizer step bumps it, so a stale copy is never used)."""
+    params = [p for p in params if p is not None and p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()]
+    L = _lib.load()
+    for i in range(0, len(params), 64):
+        chunk = params[i:i + 64]
+        offs, total = [], 0
+        for p in chunk:   # 128-byte aligned pieces (the GEMMs' operand pointers)
+            offs.append(total)
+            total += (p.numel() + 63) // 64 * 64
+        flat = torch.empty(total, device=chunk[0].device, dtype=torch.bfloat16)
+        dsts = [flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, chunk)]
+        n = len(chunk)
+        src = (ctypes.c_void_p * n)(*[p.data_ptr() for p in chunk])
+        dst = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dsts])
+        cnt = (ctypes.c_int64 * n)(*[p.numel() for p in chunk])
+        check(L.mmni_cast_bf16_multi(n, src, dst, cnt, stream_handle(chunk[0].device)), "mmni_cast_bf16_multi")
+        for p, d in zip(chunk, dsts):
+            _BF16_CACHE[(p.data_ptr(), tuple(p.shape))] = (p._version, d)
+
+
+def _autocast_copy(t, cdt):
+    """t.to(cdt), or this step's bf16 copy from cast_params_bf16 when it is current."""
+    if t is None:
+        return None
+    if cdt == torch.bfloat16 and t.dtype == torch.float32:
+        e = _BF16_CACHE.get((t.data_ptr(), tuple(t.shape)))
+        if e is not None and e[0] == t._version:
+            return e[1]
+    return t.to(cdt)
+
+
 def _splitk_wgrad(dy2, x2, dw, db):
     """dw (N, K) = dy2^T x2 and db (N) = colsum dy2 (nullable) into fp32 destinations (contiguous
     row blocks of a larger gradient are fine): the S chunk products on the library GEMM, their
@@ -1081,8 +1120,8 @@ class _InProjQKV(torch.autograd.Function):
         ctx.dtypes = (xq.dtype, xkv.dtype, weight.dtype)
         if torch.is_autocast_enabled() and xq.is_cuda:
             cdt = torch.get_autocast_dtype("cuda")
-            xq, xkv, wc = xq.to(cdt), xkv.to(cdt), weight.to(cdt)
-            bc = bias.to(cdt) if bias is not None else None
+            xq, xkv, wc = xq.to(cdt), xkv.to(cdt), _autocast_copy(weight, cdt)
+            bc = _autocast_copy(bias, cdt)
         else:
             wc, bc = weight, bias
         with torch.autocast(device_type="cuda", enabled=False):

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from .position_embedding import SinusoidalPositionalEmbedding
 from .multihead_attention import MultiheadAttention
-from ..functional import SplitKLinear, dropout_seed, encoder_layer_rows, layer_norm
+from ..functional import SplitKLinear, cast_params_bf16, dropout_seed, encoder_layer_rows, layer_norm
 
 
 class TransformerEncoder(nn.Module):
@@ -43,8 +43,17 @@ class TransformerEncoder(nn.Module):
             x = x + self.embed_positions(x_in.transpose(0, 1)[:, :, 0]).transpose(0, 1)
         return F.dropout(x, p=self.dropout, training=self.training)
 
+    def _gemm_params(self):
+        for layer in self.layers:
+            a = layer.self_attn
+            yield from (a.in_proj_weight, a.in_proj_bias, a.out_proj.weight, a.out_proj.bias, layer.fc1.weight,
+                        layer.fc1.bias, layer.fc2.weight, layer.fc2.bias)
+
     def forward(self, x_in, x_in_k=None, x_in_v=None):
         """x_in (T, B, E) [, x_in_k, x_in_v (Tk, B, E)] -> (T, B, E)."""
+        if x_in.is_cuda and torch.is_autocast_enabled() and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            # this step's bf16 copies of every layer's GEMM weights and biases in a few launches
+            cast_params_bf16(list(self._gemm_params()))
         x = self._embed(x_in)
         cross = x_in_k is not None and x_in_v is not None
         if cross:

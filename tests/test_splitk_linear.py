@@ -93,3 +93,22 @@ def test_device_reduction_fp32_matches_float64():
             assert torch.equal(a, a2)
             err = float((a.double().cpu() - r).abs().max() / r.abs().max())
             assert err < 1e-5, err
+
+
+@pytest.mark.gpu
+def test_cast_params_bf16_matches_torch_and_tracks_versions():
+    """mmni_cast_bf16_multi (70 tensors: two launches) is bit-equal to torch's .to(bfloat16); the
+    autocast Linears use a copy only while its parameter's version is unchanged."""
+    from multimodal_neuroimage_amd import functional as MF
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(3)
+    sizes = ([84 * 84, 84, 1, 336 * 84, 13, 672 * 168] * 12)[:70]
+    ps = [torch.randn(n, device=dev, generator=g) * 10 for n in sizes]
+    MF.cast_params_bf16(ps)
+    for p in ps:
+        c = MF._autocast_copy(p, torch.bfloat16)
+        assert c.shape == p.shape and torch.equal(c, p.to(torch.bfloat16))
+        assert c.data_ptr() % 128 == 0
+    p = ps[0]
+    p.add_(1.0)   # an optimizer step: version bump -> fresh cast
+    assert torch.equal(MF._autocast_copy(p, torch.bfloat16), p.to(torch.bfloat16))
