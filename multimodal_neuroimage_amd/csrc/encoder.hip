@@ -601,6 +601,113 @@ __global__ __launch_bounds__(256) void row_ln_fwd_kernel(int64_t rows, int C, co
     }
 }
 
+// Quad-lane variants for C % 4 == 0 (the crossmodal widths 84 / 168): a row takes LPR lanes (32 for
+// C <= 128, 64 for C <= 256), each holding 4 consecutive columns from one 16-byte load, so a wave
+// covers 64 / LPR rows at once (84: two rows of 21 live lanes, against one row of 64 + 20 four-byte
+// loads in the scalar kernels).  Row sums: xor butterflies inside the LPR-lane segment.
+template <typename TO>
+__device__ __forceinline__ void st4(TO* p, float a, float b, float c, float d);
+template <>
+__device__ __forceinline__ void st4<float>(float* p, float a, float b, float c, float d) {
+    *reinterpret_cast<f4*>(p) = (f4){a, b, c, d};
+}
+template <>
+__device__ __forceinline__ void st4<__bf16>(__bf16* p, float a, float b, float c, float d) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<b4*>(p) = (b4){(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+}
+template <typename TI>
+__device__ __forceinline__ f4 ld4v(const TI* p);
+template <>
+__device__ __forceinline__ f4 ld4v<float>(const float* p) { return *reinterpret_cast<const f4*>(p); }
+template <>
+__device__ __forceinline__ f4 ld4v<__bf16>(const __bf16* p) {
+    const uint2 q = *reinterpret_cast<const uint2*>(p);
+    return (f4){__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
+                __uint_as_float(q.y & 0xffff0000u)};
+}
+template <int LPR>
+__device__ __forceinline__ float seg_sum(float v) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <typename TO, int LPR>
+__global__ __launch_bounds__(256) void row_ln_fwd_q_kernel(int64_t rows, int C, const float* __restrict__ x,
+                                                           int64_t ldx, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps, TO* y,
+                                                           int64_t ldy, float* mean, float* rstd) {
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane / LPR, c0 = (lane % LPR) * 4;
+    const bool live = c0 < C;
+    const f4 gm = live ? *reinterpret_cast<const f4*>(gamma + c0) : zero4();
+    const f4 bt = live ? *reinterpret_cast<const f4*>(beta + c0) : zero4();
+    const float invC = 1.0f / (float)C;
+    for (int64_t rb = ((int64_t)blockIdx.x * 4 + wave) * RPW; rb < rows; rb += (int64_t)gridDim.x * 4 * RPW) {
+        const int64_t r = rb + sub;
+        const bool ok = live & (r < rows);
+        const f4 v = ok ? *reinterpret_cast<const f4*>(x + r * ldx + c0) : zero4();
+        const float mu = seg_sum<LPR>((v[0] + v[1]) + (v[2] + v[3])) * invC;
+        const f4 d = ok ? v - mu : zero4();
+        const float q = seg_sum<LPR>((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]));
+        const float rs = 1.0f / sqrtf(q * invC + eps);
+        if (ok)
+            st4<TO>(y + r * ldy + c0, fmaf(d[0] * rs, gm[0], bt[0]), fmaf(d[1] * rs, gm[1], bt[1]),
+                    fmaf(d[2] * rs, gm[2], bt[2]), fmaf(d[3] * rs, gm[3], bt[3]));
+        if (c0 == 0 && r < rows) {
+            mean[r] = mu;
+            rstd[r] = rs;
+        }
+    }
+}
+
+template <bool RES, typename TI, int LPR>
+__global__ __launch_bounds__(256) void row_ln_bwd_q_kernel(LNBArgs a) {
+    constexpr int RPW = 64 / LPR;
+    __shared__ f4 red[4 * RPW][2][64];
+    const TI* dxn = static_cast<const TI*>(a.dxn);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane / LPR, cq = lane % LPR, c0 = cq * 4;
+    const bool live = c0 < a.C;
+    const f4 gm = live ? *reinterpret_cast<const f4*>(a.gamma + c0) : zero4();
+    f4 dg = zero4(), db = zero4();
+    const float invC = 1.0f / (float)a.C;
+    for (int64_t rb = ((int64_t)blockIdx.x * 4 + wave) * RPW; rb < a.rows; rb += (int64_t)gridDim.x * 4 * RPW) {
+        const int64_t r = rb + sub;
+        const bool ok = live & (r < a.rows);
+        const int64_t rr = r < a.rows ? r : a.rows - 1;
+        const float m = a.mean[rr], rs = a.rstd[rr];
+        f4 d = ok ? ld4v<TI>(dxn + r * a.lddxn + c0) : zero4();
+        const f4 xv = ok ? *reinterpret_cast<const f4*>(a.x + r * a.ldx + c0) : zero4();
+        f4 rv = zero4();
+        if (RES && ok) rv = *reinterpret_cast<const f4*>(a.dres + r * a.ldres + c0);
+        const f4 xh = ok ? (xv - m) * rs : zero4();
+        const f4 gd = d * gm;
+        const float s1 = seg_sum<LPR>((gd[0] + gd[1]) + (gd[2] + gd[3])) * invC;
+        const float s2 = seg_sum<LPR>((gd[0] * xh[0] + gd[1] * xh[1]) + (gd[2] * xh[2] + gd[3] * xh[3])) * invC;
+        dg += d * xh;
+        db += d;
+        if (ok) {
+            const f4 o = rs * (gd - s1 - xh * s2) + rv;
+            *reinterpret_cast<f4*>(a.dx + r * a.lddx + c0) = o;
+        }
+    }
+    red[wave * RPW + sub][0][cq] = dg;
+    red[wave * RPW + sub][1][cq] = db;
+    __syncthreads();
+    float* p = a.part + (int64_t)blockIdx.x * 2 * a.C;
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+        float tg = 0.f, tb = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4 * RPW; ++k) {   // fixed order: wave-major, then row group
+            tg += red[k][0][c >> 2][c & 3];
+            tb += red[k][1][c >> 2][c & 3];
+        }
+        p[c] = tg;
+        p[a.C + c] = tb;
+    }
+}
+
 constexpr int kLnbBlocks = 768;   // ~2 rows per wave at 6,912 rows: a short dependent chain per wave
 
 // row chunks of a weight gradient: >= 64 rows each (4 groups per wave), at most 256, and a
@@ -734,7 +841,25 @@ int enc_row_ln_bwd_t(int64_t rows, int C, const void* dxn, int dxn_bf16, int64_t
     a.part = static_cast<float*>(workspace);
     int64_t blocks = (rows + 3) / 4;
     if (blocks > enc::kLnbBlocks) blocks = enc::kLnbBlocks;
-    if (dxn_bf16) {
+    const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool quad = C % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && lddxn % 4 == 0 &&
+                      (dres == nullptr || ldres % 4 == 0) && al16(x) && al16(dx) && al16(gamma) &&
+                      (reinterpret_cast<uintptr_t>(dxn) & (dxn_bf16 ? 7 : 15)) == 0 && (dres == nullptr || al16(dres));
+    if (quad) {
+#define MMNI_LNBQ(LPR)                                                                                          \
+    do {                                                                                                        \
+        if (dxn_bf16) {                                                                                         \
+            if (dres != nullptr) enc::row_ln_bwd_q_kernel<true, __bf16, LPR><<<(unsigned)blocks, 256, 0, s>>>(a); \
+            else enc::row_ln_bwd_q_kernel<false, __bf16, LPR><<<(unsigned)blocks, 256, 0, s>>>(a);             \
+        } else {                                                                                                \
+            if (dres != nullptr) enc::row_ln_bwd_q_kernel<true, float, LPR><<<(unsigned)blocks, 256, 0, s>>>(a);  \
+            else enc::row_ln_bwd_q_kernel<false, float, LPR><<<(unsigned)blocks, 256, 0, s>>>(a);              \
+        }                                                                                                       \
+    } while (0)
+        if (C <= 128) MMNI_LNBQ(32);
+        else MMNI_LNBQ(64);
+#undef MMNI_LNBQ
+    } else if (dxn_bf16) {
         if (dres != nullptr) enc::row_ln_bwd_kernel<true, __bf16><<<(unsigned)blocks, 256, 0, s>>>(a);
         else enc::row_ln_bwd_kernel<false, __bf16><<<(unsigned)blocks, 256, 0, s>>>(a);
     } else {
@@ -807,6 +932,24 @@ extern "C" int mmni_row_layernorm_fwd_t(int64_t rows, int C, const float* x, int
     int64_t blocks = (rows + 7) / 8;   // ~2 rows per wave
     if (blocks > 4096) blocks = 4096;
     hipStream_t s = (hipStream_t)stream;
+    const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) && al16(gamma) && al16(beta) &&
+        (reinterpret_cast<uintptr_t>(y) & (y_dtype == 1 ? 7 : 15)) == 0) {
+        int64_t qb = (rows + (C <= 128 ? 7 : 3)) / (C <= 128 ? 8 : 4);   // one row group per wave
+        if (qb > 4096) qb = 4096;
+#define MMNI_LNFQ(TO, LPR)                                                                                      \
+    enc::row_ln_fwd_q_kernel<TO, LPR><<<(unsigned)qb, 256, 0, s>>>(rows, C, x, ldx, gamma, beta, eps,             \
+                                                                   static_cast<TO*>(y), ldy, mean, rstd)
+        if (y_dtype == 1) {
+            if (C <= 128) MMNI_LNFQ(__bf16, 32);
+            else MMNI_LNFQ(__bf16, 64);
+        } else {
+            if (C <= 128) MMNI_LNFQ(float, 32);
+            else MMNI_LNFQ(float, 64);
+        }
+#undef MMNI_LNFQ
+        return launch_status("row_layernorm_fwd");
+    }
     if (y_dtype == 1)
         enc::row_ln_fwd_kernel<__bf16><<<(unsigned)blocks, 256, 0, s>>>(rows, C, x, ldx, gamma, beta, eps,
                                                                          static_cast<__bf16*>(y), ldy, mean, rstd);
