@@ -6,6 +6,7 @@ are not float32 ROCm-device tensors raise.  Outputs and saved tensors are alloca
 """
 import ctypes
 import math
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -1055,6 +1056,8 @@ def cast_params_bf16(params):
     for this step's autocast Linears (_autocast_copy hands them out while the parameter's version
     is unchanged; an optimizer step bumps it, so a stale copy is never used)."""
     params = [p for p in params if p is not None and p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()]
+    for k in [k for k, e in _BF16_CACHE.items() if e[0]() is None]:   # parameters that no longer exist
+        del _BF16_CACHE[k]
     L = _lib.load()
     for i in range(0, len(params), 64):
         chunk = params[i:i + 64]
@@ -1070,7 +1073,7 @@ def cast_params_bf16(params):
         cnt = (ctypes.c_int64 * n)(*[p.numel() for p in chunk])
         check(L.mmni_cast_bf16_multi(n, src, dst, cnt, stream_handle(chunk[0].device)), "mmni_cast_bf16_multi")
         for p, d in zip(chunk, dsts):
-            _BF16_CACHE[(p.data_ptr(), tuple(p.shape))] = (p._version, d)
+            _BF16_CACHE[(p.data_ptr(), tuple(p.shape))] = (weakref.ref(p), p._version, d)
 
 
 def _autocast_copy(t, cdt):
@@ -1079,8 +1082,8 @@ def _autocast_copy(t, cdt):
         return None
     if cdt == torch.bfloat16 and t.dtype == torch.float32:
         e = _BF16_CACHE.get((t.data_ptr(), tuple(t.shape)))
-        if e is not None and e[0] == t._version:
-            return e[1]
+        if e is not None and e[0]() is t and e[1] == t._version:   # the same live tensor, unmodified
+            return e[2]
     return t.to(cdt)
 
 
