@@ -1002,25 +1002,39 @@ class _SplitKLinear(torch.autograd.Function):
     values directly (mmni_splitk_reduce; torch's two reductions took 24 us per Linear at C5)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, relu=False):
         ctx.x_dtype = x.dtype
         if torch.is_autocast_enabled() and x.is_cuda:
             cdt = torch.get_autocast_dtype("cuda")
             xc, wc = x.to(cdt), _autocast_copy(weight, cdt)
             bc = _autocast_copy(bias, cdt)
-            with torch.autocast(device_type="cuda", enabled=False):
-                y = F.linear(xc, wc, bc)
         else:
-            xc, wc = x, weight
-            y = F.linear(x, weight, bias)
-        ctx.save_for_backward(xc, wc)
+            xc, wc, bc = x, weight, bias
+        with torch.autocast(device_type="cuda", enabled=False):
+            if relu and bc is not None and xc.is_cuda:
+                # ReLU in the GEMM's epilogue (crossmodal_transformer.py:160 F.relu(self.fc1(x)))
+                K = xc.shape[-1]
+                y = torch._addmm_activation(bc, xc.reshape(-1, K), wc.t()).view(*xc.shape[:-1], wc.shape[0])
+            else:
+                y = F.linear(xc, wc, bc)
+                if relu:
+                    y = F.relu(y)
+        if relu:
+            ctx.save_for_backward(xc, wc, y)
+        else:
+            ctx.save_for_backward(xc, wc)
+        ctx.relu = relu
         ctx.w_dtype = weight.dtype
         ctx.has_bias = bias is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        if ctx.relu:
+            x, w, y = ctx.saved_tensors
+            dy = torch.ops.aten.threshold_backward(dy, y, 0)
+        else:
+            x, w = ctx.saved_tensors
         cdt = dy.dtype
         N, K = w.shape
         dx = None
@@ -1034,7 +1048,7 @@ class _SplitKLinear(torch.autograd.Function):
             dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
             db = torch.empty(N, device=dy.device, dtype=torch.float32) if ctx.has_bias else None
             _splitk_wgrad(dy2, x2, dw, db)
-            return dx, dw.to(ctx.w_dtype), (db.to(ctx.w_dtype) if db is not None else None)
+            return dx, dw.to(ctx.w_dtype), (db.to(ctx.w_dtype) if db is not None else None), None
         # CPU tensors (the float64 gradient tests): the same chunking in torch
         acc = torch.promote_types(cdt, torch.float32)   # fp32 sums (fp64 stays fp64)
         if S > 1:
@@ -1043,7 +1057,7 @@ class _SplitKLinear(torch.autograd.Function):
         else:
             dw = (dy2.t() @ x2).to(acc)
         db = dy2.sum(0, dtype=acc).to(ctx.w_dtype) if ctx.has_bias else None
-        return dx, dw.to(ctx.w_dtype), db
+        return dx, dw.to(ctx.w_dtype), db, None
 
 
 # bf16 copies of fp32 parameters made for the current step (cast_params_bf16), looked up by the
@@ -1173,9 +1187,9 @@ def mha_packed(q_src, kv_src, heads, causal_diag=0, scale=None, dropout=0.0, see
     return _MHARows.apply(q2, kv2, Tq, Tk, B, heads, causal_diag, scale, float(dropout), int(seed or 0))
 
 
-def splitk_linear(x, weight, bias=None):
-    """F.linear with the split-K weight gradient (see _SplitKLinear)."""
-    return _SplitKLinear.apply(x, weight, bias)
+def splitk_linear(x, weight, bias=None, relu=False):
+    """F.linear (F.relu of it with relu=True) with the split-K weight gradient (see _SplitKLinear)."""
+    return _SplitKLinear.apply(x, weight, bias, relu)
 
 
 class SplitKLinear(torch.nn.Linear):

@@ -12,7 +12,8 @@ import torch.nn.functional as F
 
 from .position_embedding import SinusoidalPositionalEmbedding
 from .multihead_attention import MultiheadAttention
-from ..functional import SplitKLinear, cast_params_bf16, dropout_seed, encoder_layer_rows, layer_norm
+from ..functional import (SplitKLinear, cast_params_bf16, dropout_seed, encoder_layer_rows, layer_norm,
+                          splitk_linear)
 
 
 class TransformerEncoder(nn.Module):
@@ -127,7 +128,10 @@ class TransformerEncoderLayer(nn.Module):
         x = self.maybe_layer_norm(0, x, after=True)
         residual = x
         x = self.maybe_layer_norm(1, x, before=True)
-        x = F.relu(self.fc1(x))
+        if x.is_cuda:   # ReLU in the fc1 GEMM's epilogue
+            x = splitk_linear(x, self.fc1.weight, self.fc1.bias, relu=True)
+        else:
+            x = F.relu(self.fc1(x))
         x = F.dropout(x, p=self.relu_dropout, training=self.training)
         x = self.fc2(x)
         x = F.dropout(x, p=self.res_dropout, training=self.training)

@@ -112,3 +112,26 @@ def test_cast_params_bf16_matches_torch_and_tracks_versions():
     p = ps[0]
     p.add_(1.0)   # an optimizer step: version bump -> fresh cast
     assert torch.equal(MF._autocast_copy(p, torch.bfloat16), p.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_relu_epilogue_matches_f_relu():
+    """relu=True (the fc1 of the crossmodal layer: ReLU in the GEMM epilogue, mask from the saved
+    output in the backward) against F.relu(F.linear(...)): fp32 to 1e-5, bf16 autocast to 2e-2."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5)
+    for auto, tol in ((False, 1e-5), (True, 2e-2)):
+        x = torch.randn(4096, 2, 84, device=dev, generator=g).requires_grad_(True)
+        w = (torch.randn(336, 84, device=dev, generator=g) * 0.1).requires_grad_(True)
+        b = torch.randn(336, device=dev, generator=g).requires_grad_(True)
+        gy = torch.randn(4096, 2, 336, device=dev, generator=g)
+        outs = []
+        for fused in (True, False):
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=auto):
+                y = splitk_linear(x, w, b, relu=True) if fused else torch.relu(torch.nn.functional.linear(x, w, b))
+            y.backward(gy.to(y.dtype))
+            outs.append((y.detach().float(), x.grad.float(), w.grad.clone(), b.grad.clone()))
+            x.grad = w.grad = b.grad = None
+        for a, r in zip(*outs):
+            err = float((a - r).abs().max() / r.abs().max())
+            assert err < tol, (auto, err)
